@@ -1,0 +1,120 @@
+"""Python host mirror of the reference's render driver over the C ABI.
+
+Mirrors /root/reference/bwidman-raytracer/src/Main.cu: allocateScene()
+(:38-109) -> Renderer.set_scene(); the frame loop's render() +
+accumulatedFrames++ (:467-480) -> Renderer.render(); controls()' reset
+(Controls.cuh:15..69) -> Renderer.reset_accumulation() / set_camera().
+Every call goes to libbwrt.so (HIP); there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class Renderer:
+    def __init__(self, device: int = 0, lib=None):
+        self.lib = lib or abi.load()
+        self.ctx = C.c_void_p()
+        abi.check(self.lib, self.lib.rt_create(device, C.byref(self.ctx)))
+        self.device = device
+        self.scene = None
+
+    # -- context lifetime -------------------------------------------------
+    def close(self):
+        if self.ctx:
+            self.lib.rt_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, status):
+        return abi.check(self.lib, status, self.ctx)
+
+    # -- scene / camera / accumulation -----------------------------------
+    def set_scene(self, scene):
+        self.scene = scene
+        self._check(self.lib.rt_set_scene(self.ctx, C.byref(scene.struct)))
+
+    def set_camera(self, camera):
+        self._check(self.lib.rt_set_camera(self.ctx, C.byref(camera)))
+
+    def reset_accumulation(self):
+        self._check(self.lib.rt_reset_accumulation(self.ctx))
+
+    @property
+    def frame_counter(self) -> int:
+        return self.lib.rt_frame_counter(self.ctx)
+
+    def set_max_bounces(self, mb: int):
+        self._check(self.lib.rt_set_max_bounces(self.ctx, mb))
+
+    def init_rand(self, width, height, row_offset=0, row_stride=1):
+        self._check(self.lib.rt_init_rand(self.ctx, width, height, row_offset, row_stride))
+
+    # -- rendering ----------------------------------------------------------
+    @staticmethod
+    def params(width, height, samples, max_bounces, first_frame=0, row_offset=0, row_stride=1):
+        return abi.RenderParams(width, height, samples, max_bounces, first_frame, row_offset,
+                                row_stride)
+
+    def render_simple(self, width: int, height: int, samples: int) -> np.ndarray:
+        """Drop-in render(width, height, samples): continue accumulation."""
+        out = np.empty((height, width, 4), dtype=np.uint8)
+        self._check(self.lib.rt_render(self.ctx, width, height, samples, out.ctypes.data))
+        return out
+
+    def render(self, width, height, samples, max_bounces=abi.RT_DEFAULT_MAX_BOUNCES, first_frame=0,
+               row_offset=0, row_stride=1, want_accum=False):
+        rows = self.lib.rt_shard_rows(height, row_offset, row_stride)
+        out = np.empty((rows, width, 4), dtype=np.uint8)
+        acc = np.empty((rows, width, 3), dtype=np.float32) if want_accum else None
+        p = self.params(width, height, samples, max_bounces, first_frame, row_offset, row_stride)
+        self._check(self.lib.rt_render_ex(self.ctx, C.byref(p), out.ctypes.data,
+                                          acc.ctypes.data if acc is not None else None))
+        return (out, acc) if want_accum else out
+
+    def render_device(self, params: abi.RenderParams, rgba_ptr: int, stream_ptr: int | None = None):
+        self._check(self.lib.rt_render_device(self.ctx, C.byref(params), rgba_ptr, stream_ptr))
+
+    def synchronize(self):
+        self._check(self.lib.rt_synchronize(self.ctx))
+
+    def last_kernel_ms(self) -> float:
+        return self.lib.rt_last_kernel_ms(self.ctx)
+
+    def deinterleave_device(self, gathered_ptr, image_ptr, width, height, shards, rows_per_shard,
+                            stream_ptr=None):
+        self._check(self.lib.rt_deinterleave_rows_device(self.ctx, gathered_ptr, image_ptr, width,
+                                                         height, shards, rows_per_shard,
+                                                         stream_ptr))
+
+    # -- checkpoint / resume -----------------------------------------------
+    def get_state(self, rows, width):
+        rng = np.empty((6, rows, width), dtype=np.uint32)
+        acc = np.empty((rows, width, 3), dtype=np.float32)
+        self._check(self.lib.rt_get_state(self.ctx, rng.ctypes.data, acc.ctypes.data))
+        return rng, acc
+
+    def set_state(self, rng, acc, frame_counter):
+        rng = np.ascontiguousarray(rng, dtype=np.uint32)
+        acc = np.ascontiguousarray(acc, dtype=np.float32)
+        self._check(self.lib.rt_set_state(self.ctx, rng.ctypes.data, acc.ctypes.data,
+                                          frame_counter))
+
+
+def shard_rows(height: int, row_offset: int, row_stride: int) -> int:
+    return len(range(row_offset, height, row_stride)) if row_stride > 0 else 0

@@ -1,0 +1,557 @@
+// rt_context.cpp — implementation of the C ABI (include/rt_abi.h).
+//
+// Host-side replacement of the reference's render driver
+// (/root/reference/bwidman-raytracer/src/Main.cu:38-109 allocateScene,
+// :317-366 render, :401-496 main's state handling): the context owns the
+// device copy of the (compiled) scene, the per-pixel RNG state and frameSum
+// accumulator of one pixel-row shard, a HIP stream and timing events.
+//
+// Compiled with -ffp-contract=off: the host-side scene compilation and the
+// camera prelude (Main.cu:336-338) use the reference's float operations in
+// the reference's order, so the kernel sees bit-identical inputs.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_abi.h"
+#include "rt_layout.h"
+
+hipError_t rt_launch_render(const rt_kparams& K, int block, hipStream_t stream);
+hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
+                               hipStream_t stream);
+hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
+                                  int shards, int rows_per_shard, hipStream_t stream);
+
+static_assert(sizeof(rt_vec3) == 12, "vec3d layout (Math.cuh:35-39)");
+static_assert(sizeof(rt_material) == 24, "material layout (WorldTypes.cuh:15-20)");
+static_assert(sizeof(rt_sphere) == 40 && offsetof(rt_sphere, mat) == 16, "sphere layout");
+static_assert(sizeof(rt_plane) == 60 && offsetof(rt_plane, mat) == 36, "plane layout");
+static_assert(sizeof(rt_triangle) == 60 && offsetof(rt_triangle, mat) == 36, "triangle layout");
+static_assert(sizeof(rt_quad) == 72 && offsetof(rt_quad, mat) == 48, "quad layout");
+static_assert(sizeof(rt_camera) == 24, "camera layout (WorldTypes.cuh:9-13)");
+static_assert(sizeof(rt_scene) == 88 && offsetof(rt_scene, spheres) == 24 &&
+                  offsetof(rt_scene, sphere_count) == 32 && offsetof(rt_scene, planes) == 40 &&
+                  offsetof(rt_scene, triangles) == 56 && offsetof(rt_scene, quads) == 72 &&
+                  offsetof(rt_scene, quad_count) == 80,
+              "scene layout (WorldTypes.cuh:44-53)");
+
+namespace {
+
+struct V3 {
+    float x, y, z;
+};
+V3 v3(const rt_vec3& a) { return {a.x, a.y, a.z}; }
+V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+V3 cross(V3 a, V3 b) {  // Math.cuh:103-108
+    float i = a.y * b.z - a.z * b.y;
+    float j = -(a.x * b.z - a.z * b.x);
+    float k = a.x * b.y - a.y * b.x;
+    return {i, j, k};
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct rt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    std::string err;
+
+    // compiled scene
+    bool has_scene = false;
+    rt_camera camera{};
+    int n_sph = 0, n_pln = 0, n_tri = 0, n_quad = 0;
+    DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table
+    size_t off_pln = 0, off_tri = 0, off_quad = 0, off_hit = 0;  // in floats
+
+    // shard state
+    int width = 0, height = 0, row_offset = 0, row_stride = 1, rows = 0;
+    DevBuf rng, accum, rgba;
+    unsigned frame = 1;
+    int max_bounces = RT_DEFAULT_MAX_BOUNCES;
+};
+
+namespace {
+
+int fail(rt_context* c, int code, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+int hip_fail(rt_context* c, hipError_t e, const char* what) {
+    return fail(c, e == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_HIP, "%s: %s", what,
+                hipGetErrorString(e));
+}
+
+#define HIP_TRY(ctx, expr)                                  \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return hip_fail(ctx, _e, #expr); \
+    } while (0)
+
+void free_buf(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+int ensure_buf(rt_context* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return RT_OK;
+    free_buf(b);
+    if (bytes == 0) return RT_OK;
+    HIP_TRY(c, hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+    return RT_OK;
+}
+
+int shard_rows(int height, int row_offset, int row_stride) {
+    if (height <= 0 || row_offset < 0 || row_stride <= 0 || row_offset >= height) return 0;
+    return (height - row_offset + row_stride - 1) / row_stride;
+}
+
+void put_material(float* h, const rt_material& m) {
+    h[4] = m.albedo.x;
+    h[5] = m.albedo.y;
+    h[6] = m.albedo.z;
+    h[7] = m.emittance;
+    h[8] = m.roughness;
+    // fresnel(): square(ior)/square(1.0f) - 1.0f (Main.cu:125)
+    h[9] = (m.refractive_index * m.refractive_index) / (1.0f * 1.0f) - 1.0f;
+    h[10] = 0.0f;
+    h[11] = 0.0f;
+}
+
+// Triangle / quad record: {n, d, v0, in0, v1, in1, ...}; Intersection.cuh:109-127
+void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_material& m) {
+    V3 v[4], e[4];
+    for (int k = 0; k < nv; k++) v[k] = v3(verts[k]);
+    for (int k = 0; k < nv; k++) e[k] = sub(v[(k + 1) % nv], v[k]);
+    V3 n = cross(e[0], e[1]);   // plane {v0, {e0, e1}}: normal = cross(d0, d1)
+    float d = -dot(n, v[0]);    // Intersection.cuh:83
+    q[0] = n.x;
+    q[1] = n.y;
+    q[2] = n.z;
+    q[3] = d;
+    for (int k = 0; k < nv; k++) {
+        V3 in = cross(n, e[k]);  // Intersection.cuh:125-127
+        float* r = q + 4 + 6 * k;
+        r[0] = v[k].x;
+        r[1] = v[k].y;
+        r[2] = v[k].z;
+        r[3] = in.x;
+        r[4] = in.y;
+        r[5] = in.z;
+    }
+    h[0] = n.x;
+    h[1] = n.y;
+    h[2] = n.z;
+    h[3] = 0.0f;
+    put_material(h, m);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_version(void) { return "0.1.0"; }
+
+rt_material rt_material_default(void) {
+    rt_material m;
+    m.albedo = {0.0f, 0.0f, 0.0f};
+    m.emittance = 0.0f;
+    m.roughness = 1.0f;
+    m.refractive_index = 1.05f;  // WorldTypes.cuh:19 (double 1.05 -> float)
+    return m;
+}
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rt_create(int device, rt_context** out) {
+    if (!out) return RT_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return RT_ERR_INVALID_ARGUMENT;
+    rt_context* c = new rt_context();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return RT_ERR_HIP;
+    }
+    c->last_stream = c->stream;
+    *out = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_context* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->last_stream && c->last_stream != c->stream) (void)hipStreamSynchronize(c->last_stream);
+    free_buf(c->scene_buf);
+    free_buf(c->rng);
+    free_buf(c->accum);
+    free_buf(c->rgba);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int rt_set_scene(rt_context* c, const rt_scene* s) {
+    if (!c || !s) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (s->sphere_count < 0 || s->plane_count < 0 || s->triangle_count < 0 || s->quad_count < 0)
+        return fail(c, RT_ERR_INVALID_ARGUMENT, "negative primitive count");
+    if ((s->sphere_count && !s->spheres) || (s->plane_count && !s->planes) ||
+        (s->triangle_count && !s->triangles) || (s->quad_count && !s->quads))
+        return fail(c, RT_ERR_INVALID_ARGUMENT, "null primitive array with non-zero count");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int ns = s->sphere_count, np = s->plane_count, nt = s->triangle_count, nq = s->quad_count;
+    const size_t off_pln = (size_t)ns * RT_SPH_FLOATS;
+    const size_t off_tri = off_pln + (size_t)np * RT_PLN_FLOATS;
+    const size_t off_quad = off_tri + (size_t)nt * RT_TRI_FLOATS;
+    const size_t off_hit = off_quad + (size_t)nq * RT_QUAD_FLOATS;
+    const size_t total = off_hit + (size_t)(ns + np + nt + nq) * RT_HIT_FLOATS + 4;
+    std::vector<float> h(total, 0.0f);
+    float* hit = h.data() + off_hit;
+    int id = 0;
+    for (int i = 0; i < ns; i++, id++) {  // Intersection.cuh:32-38
+        const rt_sphere& sp = s->spheres[i];
+        float* q = h.data() + (size_t)i * RT_SPH_FLOATS;
+        q[0] = sp.position.x;
+        q[1] = sp.position.y;
+        q[2] = sp.position.z;
+        q[3] = sp.radius * sp.radius;
+        float* hh = hit + (size_t)id * RT_HIT_FLOATS;
+        hh[0] = sp.position.x;
+        hh[1] = sp.position.y;
+        hh[2] = sp.position.z;
+        hh[3] = 1.0f;  // sphere: normal = normalize(P - centre)
+        put_material(hh, sp.mat);
+    }
+    for (int i = 0; i < np; i++, id++) {  // Intersection.cuh:69,83
+        const rt_plane& pl = s->planes[i];
+        V3 n = cross(v3(pl.directions[0]), v3(pl.directions[1]));
+        float d = -dot(n, v3(pl.origin));
+        float* q = h.data() + off_pln + (size_t)i * RT_PLN_FLOATS;
+        q[0] = n.x;
+        q[1] = n.y;
+        q[2] = n.z;
+        q[3] = d;
+        float* hh = hit + (size_t)id * RT_HIT_FLOATS;
+        hh[0] = n.x;
+        hh[1] = n.y;
+        hh[2] = n.z;
+        hh[3] = 0.0f;
+        put_material(hh, pl.mat);
+    }
+    for (int i = 0; i < nt; i++, id++)
+        compile_polygon(h.data() + off_tri + (size_t)i * RT_TRI_FLOATS, hit + (size_t)id * RT_HIT_FLOATS,
+                        s->triangles[i].vertices, 3, s->triangles[i].mat);
+    for (int i = 0; i < nq; i++, id++)
+        compile_polygon(h.data() + off_quad + (size_t)i * RT_QUAD_FLOATS, hit + (size_t)id * RT_HIT_FLOATS,
+                        s->quads[i].vertices, 4, s->quads[i].mat);
+    int rc = ensure_buf(c, c->scene_buf, total * sizeof(float));
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpyAsync(c->scene_buf.p, h.data(), total * sizeof(float), hipMemcpyHostToDevice,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->n_sph = ns;
+    c->n_pln = np;
+    c->n_tri = nt;
+    c->n_quad = nq;
+    c->off_pln = off_pln;
+    c->off_tri = off_tri;
+    c->off_quad = off_quad;
+    c->off_hit = off_hit;
+    c->camera = s->camera;
+    c->has_scene = true;
+    c->frame = 1;
+    return RT_OK;
+}
+
+int rt_set_camera(rt_context* c, const rt_camera* cam) {
+    if (!c || !cam) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
+    c->camera = *cam;
+    c->frame = 1;  // Controls.cuh: any movement sets accumulatedFrames = 1
+    return RT_OK;
+}
+
+int rt_reset_accumulation(rt_context* c) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    c->frame = 1;
+    return RT_OK;
+}
+
+unsigned rt_frame_counter(const rt_context* c) { return c ? c->frame : 0u; }
+
+int rt_set_max_bounces(rt_context* c, int mb) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    if (mb < 0) return fail(c, RT_ERR_INVALID_ARGUMENT, "max_bounces < 0");
+    if (mb > RT_MAX_BOUNCES) return fail(c, RT_ERR_UNSUPPORTED, "max_bounces > %d", RT_MAX_BOUNCES);
+    c->max_bounces = mb;
+    return RT_OK;
+}
+
+int rt_shard_rows(int height, int row_offset, int row_stride) {
+    return shard_rows(height, row_offset, row_stride == 0 ? 1 : row_stride);
+}
+
+int rt_init_rand(rt_context* c, int width, int height, int row_offset, int row_stride) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    if (row_stride == 0) row_stride = 1;
+    if (width <= 0 || height <= 0 || row_offset < 0 || row_stride < 0 || row_offset >= height)
+        return fail(c, RT_ERR_INVALID_ARGUMENT, "bad shard %dx%d offset %d stride %d", width, height,
+                    row_offset, row_stride);
+    if ((long long)width * height > (1ll << 31))
+        return fail(c, RT_ERR_UNSUPPORTED, "image larger than 2^31 pixels");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int rows = shard_rows(height, row_offset, row_stride);
+    const size_t npix = (size_t)rows * width;
+    int rc = ensure_buf(c, c->rng, npix * 6 * sizeof(unsigned));
+    if (!rc) rc = ensure_buf(c, c->accum, npix * 3 * sizeof(float));
+    if (rc) return rc;
+    HIP_TRY(c, hipMemsetAsync(c->accum.p, 0, npix * 3 * sizeof(float), c->stream));
+    HIP_TRY(c, rt_launch_init_rand((unsigned*)c->rng.p, width, rows, row_offset, row_stride, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->width = width;
+    c->height = height;
+    c->row_offset = row_offset;
+    c->row_stride = row_stride;
+    c->rows = rows;
+    c->frame = 1;
+    return RT_OK;
+}
+
+static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsigned& first) {
+    if (!c || !p) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "rt_set_scene() not called");
+    const int stride = p->row_stride == 0 ? 1 : p->row_stride;
+    if (p->width <= 0 || p->height <= 0 || p->samples <= 0 || p->row_offset < 0 || stride < 0 ||
+        p->row_offset >= p->height)
+        return fail(c, RT_ERR_INVALID_ARGUMENT, "bad render params %dx%d samples %d shard %d/%d", p->width,
+                    p->height, p->samples, p->row_offset, stride);
+    if (p->max_bounces < 0) return fail(c, RT_ERR_INVALID_ARGUMENT, "max_bounces < 0");
+    if (p->max_bounces > RT_MAX_BOUNCES)
+        return fail(c, RT_ERR_UNSUPPORTED, "max_bounces %d > %d", p->max_bounces, RT_MAX_BOUNCES);
+    if (c->width != p->width || c->height != p->height || c->row_offset != p->row_offset ||
+        c->row_stride != stride || !c->rng.p) {
+        int rc = rt_init_rand(c, p->width, p->height, p->row_offset, stride);
+        if (rc) return rc;
+    }
+    first = p->first_frame ? p->first_frame : c->frame;
+    if ((unsigned long long)first + (unsigned)p->samples > 0xffffffffull)
+        return fail(c, RT_ERR_INVALID_ARGUMENT, "frame counter overflow");
+    HIP_TRY(c, hipSetDevice(c->device));
+
+    std::memset(&K, 0, sizeof K);
+    K.width = p->width;
+    K.height = p->height;
+    K.row_offset = p->row_offset;
+    K.row_stride = stride;
+    K.rows = c->rows;
+    K.samples = p->samples;
+    K.max_bounces = p->max_bounces;
+    K.first_frame = first;
+    // host prelude, Main.cu:336-338
+    const rt_camera& cam = c->camera;
+    K.cam_pos[0] = cam.position.x;
+    K.cam_pos[1] = cam.position.y;
+    K.cam_pos[2] = cam.position.z;
+    K.screen_z = -(float)(p->width / 2) / tanf(cam.fov / 2.0f);
+    {
+        const float cy = cosf(cam.angle[0]), sy = sinf(cam.angle[0]);  // rotationMatrix3DY
+        const float cx = cosf(cam.angle[1]), sx = sinf(cam.angle[1]);  // rotationMatrix3DX
+        const float L[3][3] = {{cy, 0, sy}, {0, 1, 0}, {-sy, 0, cy}};
+        const float U[3][3] = {{1, 0, 0}, {0, cx, -sx}, {0, sx, cx}};
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++)  // dot(a.row(i), b.col(j)), Math.cuh:191-199
+                K.rot[3 * i + j] = L[i][0] * U[0][j] + L[i][1] * U[1][j] + L[i][2] * U[2][j];
+    }
+    K.jitter = (float)(0.001 * (p->width / 1000));  // Main.cu:291
+    K.n_sph = c->n_sph;
+    K.n_pln = c->n_pln;
+    K.n_tri = c->n_tri;
+    K.n_quad = c->n_quad;
+    int nmax = c->n_sph;  // Main.cu:217
+    if (c->n_pln > nmax) nmax = c->n_pln;
+    if (c->n_tri > nmax) nmax = c->n_tri;
+    if (c->n_quad > nmax) nmax = c->n_quad;
+    K.n_max = nmax;
+    const float* base = (const float*)c->scene_buf.p;
+    K.sph = base;
+    K.pln = base + c->off_pln;
+    K.tri = base + c->off_tri;
+    K.quad = base + c->off_quad;
+    K.hit = base + c->off_hit;
+    K.rng = (unsigned*)c->rng.p;
+    K.accum = (float*)c->accum.p;
+    return RT_OK;
+}
+
+static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
+    const int block = (K.max_bounces + 1) * 7 * 256 * 4 <= 65536 ? 256 : 64;
+    HIP_TRY(c, hipEventRecord(c->ev0, s));
+    hipError_t e = rt_launch_render(K, block, s);
+    if (e != hipSuccess) return hip_fail(c, e, "rt_render_kernel launch");
+    HIP_TRY(c, hipEventRecord(c->ev1, s));
+    c->timed = true;
+    c->last_stream = s;
+    c->frame = first + (unsigned)samples;  // Main.cu:480 accumulatedFrames++
+    return RT_OK;
+}
+
+int rt_render_ex(rt_context* c, const rt_render_params* p, uint8_t* rgba_out, float* accum_out) {
+    rt_kparams K;
+    unsigned first = 0;
+    int rc = prepare(c, p, K, first);
+    if (rc) return rc;
+    const size_t npix = (size_t)c->rows * c->width;
+    rc = ensure_buf(c, c->rgba, npix * 4);
+    if (rc) return rc;
+    K.rgba = (unsigned*)c->rgba.p;
+    rc = launch(c, K, c->stream, first, p->samples);
+    if (rc) return rc;
+    if (rgba_out) HIP_TRY(c, hipMemcpyAsync(rgba_out, c->rgba.p, npix * 4, hipMemcpyDeviceToHost, c->stream));
+    if (accum_out) {
+        std::vector<float> planes(npix * 3);
+        HIP_TRY(c, hipMemcpyAsync(planes.data(), c->accum.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (size_t i = 0; i < npix; i++)
+            for (int ch = 0; ch < 3; ch++) accum_out[3 * i + ch] = planes[ch * npix + i];
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_render(rt_context* c, int width, int height, int samples, uint8_t* rgba_out) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    rt_render_params p;
+    p.width = width;
+    p.height = height;
+    p.samples = samples;
+    p.max_bounces = c->max_bounces;
+    p.first_frame = 0;
+    p.row_offset = 0;
+    p.row_stride = 1;
+    return rt_render_ex(c, &p, rgba_out, nullptr);
+}
+
+int rt_render_device(rt_context* c, const rt_render_params* p, void* rgba_device, void* stream) {
+    rt_kparams K;
+    unsigned first = 0;
+    int rc = prepare(c, p, K, first);
+    if (rc) return rc;
+    if (rgba_device && ((uintptr_t)rgba_device & 3u))
+        return fail(c, RT_ERR_INVALID_ARGUMENT, "rgba_device not 4-byte aligned");
+    K.rgba = (unsigned*)rgba_device;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, K, s, first, p->samples);
+}
+
+int rt_synchronize(rt_context* c) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->last_stream && c->last_stream != c->stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+    return RT_OK;
+}
+
+float rt_last_kernel_ms(rt_context* c) {
+    if (!c || !c->timed) return -1.0f;
+    if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+int rt_deinterleave_rows_device(rt_context* c, const void* gathered, void* image, int width, int height,
+                                int shards, int rows_per_shard, void* stream) {
+    if (!c || !gathered || !image) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (width <= 0 || height <= 0 || shards <= 0 || rows_per_shard * shards < height)
+        return fail(c, RT_ERR_INVALID_ARGUMENT, "bad deinterleave geometry");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIP_TRY(c, rt_launch_deinterleave((const unsigned*)gathered, (unsigned*)image, width, height, shards,
+                                      rows_per_shard, s));
+    c->last_stream = s;
+    return RT_OK;
+}
+
+int rt_get_state(rt_context* c, uint32_t* rng, float* accum) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    if (!c->rng.p) return fail(c, RT_ERR_INVALID_ARGUMENT, "no shard state (render or rt_init_rand first)");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->last_stream != c->stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+    const size_t npix = (size_t)c->rows * c->width;
+    if (rng) HIP_TRY(c, hipMemcpy(rng, c->rng.p, npix * 6 * sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (accum) {
+        std::vector<float> planes(npix * 3);
+        HIP_TRY(c, hipMemcpy(planes.data(), c->accum.p, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < npix; i++)
+            for (int ch = 0; ch < 3; ch++) accum[3 * i + ch] = planes[ch * npix + i];
+    }
+    return RT_OK;
+}
+
+int rt_set_state(rt_context* c, const uint32_t* rng, const float* accum, unsigned frame_counter) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    if (!c->rng.p) return fail(c, RT_ERR_INVALID_ARGUMENT, "no shard state (rt_init_rand first)");
+    if (frame_counter == 0) return fail(c, RT_ERR_INVALID_ARGUMENT, "frame_counter must be >= 1");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const size_t npix = (size_t)c->rows * c->width;
+    if (rng) HIP_TRY(c, hipMemcpy(c->rng.p, rng, npix * 6 * sizeof(unsigned), hipMemcpyHostToDevice));
+    if (accum) {
+        std::vector<float> planes(npix * 3);
+        for (size_t i = 0; i < npix; i++)
+            for (int ch = 0; ch < 3; ch++) planes[ch * npix + i] = accum[3 * i + ch];
+        HIP_TRY(c, hipMemcpy(c->accum.p, planes.data(), npix * 3 * sizeof(float), hipMemcpyHostToDevice));
+    }
+    c->frame = frame_counter;
+    return RT_OK;
+}
+
+const char* rt_error_string(int status) {
+    switch (status) {
+        case RT_OK: return "ok";
+        case RT_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case RT_ERR_NO_DEVICE: return "no HIP device";
+        case RT_ERR_HIP: return "HIP runtime error";
+        case RT_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case RT_ERR_NO_SCENE: return "no scene";
+        case RT_ERR_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+const char* rt_last_error(const rt_context* c) { return c ? c->err.c_str() : ""; }
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// rt_layout.h — device-side data layout shared by the host scene compiler
+// (rt_context.cpp) and the HIP kernels (rt_kernels.hip).
+//
+// The scene is "compiled" once on upload: every quantity the reference
+// recomputes per ray but that depends only on the primitive (plane normal
+// cross(d0,d1) Intersection.cuh:69, d = -dot(n,origin) :83, triangle/quad
+// edges + normal + inner edge normals :109-127 / :142-162, r*r :38,
+// ior^2/1^2 - 1 Main.cu:125) is precomputed with the SAME float operations
+// in the same order, so the per-ray arithmetic stays bit-identical to the
+// reference semantics while doing less work.
+//
+// HBM layout (all float32, records padded to 16 B):
+//   spheres   : n_sph  x  4 floats  {cx, cy, cz, r*r}
+//   planes    : n_pln  x  4 floats  {nx, ny, nz, d}
+//   triangles : n_tri  x 24 floats  {nx,ny,nz,d, v0[3],in0[3], v1[3],in1[3], v2[3],in2[3], pad2}
+//   quads     : n_quad x 28 floats  {nx,ny,nz,d, v0[3],in0[3], .. v3[3],in3[3]}
+//   hit table : n_prim x 12 floats  {n_or_centre[3], is_sphere,
+//                                    albedo[3], emittance,
+//                                    roughness, ior^2-1, 0, 0}
+//   primitive id = index within its kind + kind offset, kinds ordered
+//   spheres, planes, triangles, quads.
+//
+// Per-pixel progressive state (SoA planes over the shard's pixels
+// p = j*width + x, so a wave's 64 lanes touch 256 contiguous bytes):
+//   rng   : 6 planes of u32 {d, v0, v1, v2, v3, v4}   (24 B/pixel)
+//   accum : 3 planes of f32 {r, g, b}                 (12 B/pixel)
+//   rgba  : 1 plane of u32 (bytes r,g,b,255)          ( 4 B/pixel)
+#pragma once
+
+#define RT_SPH_FLOATS 4
+#define RT_PLN_FLOATS 4
+#define RT_TRI_FLOATS 24
+#define RT_QUAD_FLOATS 28
+#define RT_HIT_FLOATS 12
+
+#define RT_NEAR_ZERO 0.0001f       // Intersection.cuh:4
+#define RT_SPECULAR_CHANCE 0.5f    // Main.cu:29
+#define RT_PI 3.1415926535f        // Math.cuh:5
+
+struct rt_kparams {
+    int width, height;          // full image
+    int row_offset, row_stride; // shard rows y = row_offset + j*row_stride
+    int rows;                   // shard rows
+    int samples;                // progressive frames in this launch
+    int max_bounces;
+    unsigned first_frame;
+    float cam_pos[3];
+    float rot[9];               // rotationMatrix3DY(a0) * rotationMatrix3DX(a1), row-major
+    float screen_z;             // Main.cu:336
+    float jitter;               // (float)(0.001 * (width / 1000)), Main.cu:291
+    int n_sph, n_pln, n_tri, n_quad, n_max;
+    const float* sph;
+    const float* pln;
+    const float* tri;
+    const float* quad;
+    const float* hit;
+    unsigned* rng;              // 6 planes of rows*width
+    float* accum;               // 3 planes of rows*width
+    unsigned* rgba;             // rows*width (may be null)
+};

@@ -1,0 +1,245 @@
+/*
+ * rt_abi.h — C ABI of the MI355X-native path tracer (libbwrt.so).
+ *
+ * This is the drop-in boundary for the reference renderer's hot path
+ * (IndaPlus22/bwidman-raytracer, paths relative to /root/reference):
+ *
+ *   reference                                   | replaced by
+ *   --------------------------------------------+-----------------------------------------
+ *   structs vec3d/material/sphere/plane/        | rt_vec3 / rt_material / rt_sphere /
+ *   triangle/quad/camera/scene                  | rt_plane / rt_triangle / rt_quad /
+ *   (Math.cuh:35-39, WorldTypes.cuh:9-53)       | rt_camera / rt_scene (byte-compatible)
+ *   scene allocateScene()  (Main.cu:38-109)     | rt_set_scene()  (library uploads a copy)
+ *   initializeRand<<<>>>   (Main.cu:369-380)    | done lazily by the first render of a frame
+ *   cudaMalloc randStates/frameSum              |   size (rt_init_rand() forces it)
+ *   (Main.cu:460-465)                           |
+ *   render(scene,grid,block,cell,randStates,    | rt_render() / rt_render_ex() /
+ *          accumulatedFrames,frameSum)          | rt_render_device()
+ *   (Main.cu:317-366, kernel Main.cu:274-315)   |
+ *   accumulatedFrames++ / controls() reset      | frame counter kept in the context;
+ *   (Main.cu:467,480; Controls.cuh:15..69)      | rt_reset_accumulation(), rt_set_camera()
+ *
+ * Conventions
+ *  - Every function returns RT_OK (0) or a negative rt_status; no exceptions
+ *    cross the ABI.  rt_last_error() gives a human-readable message.
+ *  - One context = one GPU (HIP device) and one pixel-row shard.  A context
+ *    must be used by one host thread at a time.  All calls except
+ *    rt_render_device()/rt_deinterleave_rows_device() are synchronous.
+ *  - Output RGBA8 buffers are row-major, row 0 = BOTTOM of the screen
+ *    (the reference draws texcoord (0,0) at the bottom-left, Main.cu:358).
+ *  - Semantics of one "sample" (progressive frame) follow the reference
+ *    exactly: jittered camera ray, one path of up to max_bounces+1
+ *    closest-hit queries, frameSum reset when the frame number is 1,
+ *    frameSum/n -> ACES -> gamma -> *255 -> round -> u8.
+ *  - The per-pixel RNG is cuRAND-XORWOW seeded with the global pixel index
+ *    y*width+x (Main.cu:377); results are independent of sharding.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define RT_API __attribute__((visibility("default")))
+#else
+#define RT_API
+#endif
+
+/* ---- world types (byte-compatible with the reference) ------------------ */
+
+/* Math.cuh:35-39 (vec3d, also used as `color`): 12 bytes */
+typedef struct rt_vec3 {
+    float x, y, z;
+} rt_vec3;
+
+/* WorldTypes.cuh:15-20: 24 bytes.
+ * Reference defaults: albedo {0,0,0}, emittance 0, roughness 1,
+ * refractiveIndex 1.05 (see rt_material_default()). */
+typedef struct rt_material {
+    rt_vec3 albedo;
+    float emittance;
+    float roughness;
+    float refractive_index;
+} rt_material;
+
+/* WorldTypes.cuh:22-26: 40 bytes (mat at offset 16) */
+typedef struct rt_sphere {
+    rt_vec3 position;
+    float radius;
+    rt_material mat;
+} rt_sphere;
+
+/* WorldTypes.cuh:28-32: 60 bytes (mat at offset 36).
+ * The plane normal is cross(directions[0], directions[1]), NOT normalised
+ * (Intersection.cuh:69). */
+typedef struct rt_plane {
+    rt_vec3 origin;
+    rt_vec3 directions[2];
+    rt_material mat;
+} rt_plane;
+
+/* WorldTypes.cuh:34-37: 60 bytes */
+typedef struct rt_triangle {
+    rt_vec3 vertices[3];
+    rt_material mat;
+} rt_triangle;
+
+/* WorldTypes.cuh:39-42: 72 bytes */
+typedef struct rt_quad {
+    rt_vec3 vertices[4];
+    rt_material mat;
+} rt_quad;
+
+/* WorldTypes.cuh:9-13: 24 bytes.  angle[0] = yaw (RotY), angle[1] = pitch
+ * (RotX), fov in radians (horizontal). */
+typedef struct rt_camera {
+    rt_vec3 position;
+    float angle[2];
+    float fov;
+} rt_camera;
+
+/* WorldTypes.cuh:44-53: 88 bytes on LP64 (same offsets).  Unlike the
+ * reference (device pointers produced by allocateScene), the pointers here
+ * are HOST pointers: rt_set_scene() copies the arrays to the GPU; the caller
+ * keeps ownership of its arrays. */
+typedef struct rt_scene {
+    rt_camera camera;
+    const rt_sphere* spheres;
+    int sphere_count;
+    const rt_plane* planes;
+    int plane_count;
+    const rt_triangle* triangles;
+    int triangle_count;
+    const rt_quad* quads;
+    int quad_count;
+} rt_scene;
+
+/* ---- status codes ------------------------------------------------------- */
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARGUMENT = -1,
+    RT_ERR_NO_DEVICE = -2,
+    RT_ERR_HIP = -3,         /* a HIP runtime call or kernel launch failed */
+    RT_ERR_OUT_OF_MEMORY = -4,
+    RT_ERR_NO_SCENE = -5,    /* render before rt_set_scene()              */
+    RT_ERR_UNSUPPORTED = -6  /* e.g. max_bounces above RT_MAX_BOUNCES      */
+} rt_status;
+
+#define RT_MAX_BOUNCES 32
+#define RT_DEFAULT_MAX_BOUNCES 5 /* Main.cu:26 */
+
+/* Render request for the extended entry points. */
+typedef struct rt_render_params {
+    int width;          /* full image width  (Main.cu:23, windowWidth)  */
+    int height;         /* full image height (Main.cu:24, windowHeight) */
+    int samples;        /* progressive frames rendered by this call (>=1)  */
+    int max_bounces;    /* Main.cu:26; B allows B+1 closest-hit queries    */
+    unsigned first_frame; /* accumulatedFrames of the first frame of this
+                             call; 1 restarts accumulation (Main.cu:301);
+                             0 = continue from the context's frame counter */
+    int row_offset;     /* shard: render global rows y = row_offset +      */
+    int row_stride;     /*        j*row_stride, j = 0..rows-1 (0,1 = all)  */
+} rt_render_params;
+
+/* ---- context ------------------------------------------------------------ */
+
+typedef struct rt_context rt_context;
+
+/* Library / ABI version, "major.minor.patch". */
+RT_API const char* rt_version(void);
+
+/* Reference material defaults (WorldTypes.cuh:16-19). */
+RT_API rt_material rt_material_default(void);
+
+/* Number of visible HIP devices (0 when none; never fails). */
+RT_API int rt_device_count(void);
+
+/* Create a context on HIP device `device`. */
+RT_API int rt_create(int device, rt_context** out);
+RT_API void rt_destroy(rt_context* ctx);
+
+/* Upload a copy of the scene (≈ allocateScene, Main.cu:38-109).  Resets the
+ * frame counter to 1, like any camera change in controls(). */
+RT_API int rt_set_scene(rt_context* ctx, const rt_scene* scene);
+
+/* Move the camera (controls(), Controls.cuh:5-75): resets accumulation. */
+RT_API int rt_set_camera(rt_context* ctx, const rt_camera* camera);
+
+/* accumulatedFrames = 1 (Controls.cuh:15..69).  RNG streams continue. */
+RT_API int rt_reset_accumulation(rt_context* ctx);
+
+/* The frame number the next continuing render will use (accumulatedFrames). */
+RT_API unsigned rt_frame_counter(const rt_context* ctx);
+
+/* Default max_bounces for rt_render() (initially RT_DEFAULT_MAX_BOUNCES). */
+RT_API int rt_set_max_bounces(rt_context* ctx, int max_bounces);
+
+/* Allocate and seed the per-pixel state for a (width,height) image shard:
+ * curand_init(y*width+x, 0, 0) per pixel (Main.cu:369-380) and a frameSum
+ * buffer (Main.cu:464-465).  Called implicitly by the render entry points
+ * when the shard changes; calling it again reseeds the RNG. */
+RT_API int rt_init_rand(rt_context* ctx, int width, int height,
+                        int row_offset, int row_stride);
+
+/* Drop-in render(width, height, samples): renders `samples` progressive
+ * frames continuing the context's frame counter, with the context's
+ * max_bounces, over the full image, and writes the final RGBA8 image
+ * (width*height*4 bytes, row 0 = bottom) to host memory.  rgba_out may be
+ * NULL. */
+RT_API int rt_render(rt_context* ctx, int width, int height, int samples,
+                     uint8_t* rgba_out);
+
+/* Extended synchronous render.  Output rows are the shard's rows in order
+ * (rows = number of y with y = row_offset + j*row_stride < height).
+ * rgba_out: rows*width*4 bytes or NULL; accum_out: rows*width*3 floats
+ * (frameSum, interleaved r,g,b) or NULL. */
+RT_API int rt_render_ex(rt_context* ctx, const rt_render_params* p,
+                        uint8_t* rgba_out, float* accum_out);
+
+/* Asynchronous render into DEVICE memory (rows*width*4 bytes, 4-byte
+ * aligned) on HIP stream `stream` (hipStream_t; NULL = the context's own
+ * stream).  Returns after the launch; the frame counter advances. */
+RT_API int rt_render_device(rt_context* ctx, const rt_render_params* p,
+                            void* rgba_device, void* stream);
+
+/* Wait for all work of the context (its stream and the last stream passed
+ * to rt_render_device). */
+RT_API int rt_synchronize(rt_context* ctx);
+
+/* Duration (ms, HIP events on the launch stream) of the last render kernel
+ * launch; -1 when unavailable.  Synchronises on that launch's end event. */
+RT_API float rt_last_kernel_ms(rt_context* ctx);
+
+/* Number of pixel rows in the shard (row_offset, row_stride) of `height`. */
+RT_API int rt_shard_rows(int height, int row_offset, int row_stride);
+
+/* Multi-GPU gather epilogue: `gathered` holds `shards` consecutive blocks
+ * of rows_per_shard*width RGBA8 pixels, block r = rows r, r+shards, ...
+ * (row_stride = shards) padded to rows_per_shard.  Writes the full
+ * height*width image to `image` (both device pointers) on `stream`. */
+RT_API int rt_deinterleave_rows_device(rt_context* ctx, const void* gathered,
+                                       void* image, int width, int height,
+                                       int shards, int rows_per_shard,
+                                       void* stream);
+
+/* Checkpoint / resume of the progressive state of the current shard.
+ * rng: 6*rows*width uint32 as planes (d, v0..v4), accum: 3*rows*width floats
+ * interleaved r,g,b.  Either pointer may be NULL. */
+RT_API int rt_get_state(rt_context* ctx, uint32_t* rng, float* accum);
+RT_API int rt_set_state(rt_context* ctx, const uint32_t* rng,
+                        const float* accum, unsigned frame_counter);
+
+RT_API const char* rt_error_string(int status);
+RT_API const char* rt_last_error(const rt_context* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_ABI_H */

@@ -1,0 +1,39 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "bwidman-raytracer_amd"), os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libbwrt.so / HIP)")
+    config.addinivalue_line("markers", "slow: long CPU oracle runs")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as O  # tests may use the oracle (checker only)
+    O.build()
+    return O
+
+
+@pytest.fixture(scope="session")
+def bwrt_lib():
+    from bwrt import abi
+    return abi.load()  # raises if libbwrt.so is missing: no fallback
+
+
+@pytest.fixture(scope="session")
+def gpu(bwrt_lib):
+    from bwrt import Renderer
+    if bwrt_lib.rt_device_count() <= 0:
+        pytest.fail("no HIP device visible: GPU tests must run on an MI355X")
+    r = Renderer(0, lib=bwrt_lib)
+    yield r
+    r.close()

@@ -1,0 +1,195 @@
+"""GPU parity: the HIP path (libbwrt.so via the C ABI) against the oracle.
+
+Bar: bit-exact.  Both sides evaluate the reference's float operations in the
+reference's order with one IEEE-754 rounding each (no FMA contraction,
+correctly rounded div/sqrt, the same transcendental sequence), and the RNG
+is integer work, so RGBA8 output, frameSum accumulators and RNG states must
+be identical (NaN accumulators compare equal to NaN).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from bwrt import scenes
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def same_state(gpu, st_oracle):
+    rows, w = st_oracle.rows, st_oracle.width
+    rng, acc = gpu.get_state(rows, w)
+    assert np.array_equal(rng, st_oracle.rng), "RNG state differs"
+    assert np.array_equal(acc, st_oracle.accum, equal_nan=True), \
+        f"accum differs at {np.argwhere(~((acc == st_oracle.accum) | (np.isnan(acc) & np.isnan(st_oracle.accum))))[:5]}"
+
+
+def run_pair(gpu, oracle, scene, w, h, spp, mb, row_offset=0, row_stride=1):
+    gpu.set_scene(scene)
+    img = gpu.render(w, h, spp, mb, first_frame=1, row_offset=row_offset, row_stride=row_stride)
+    st = oracle.OracleState(w, h, row_offset, row_stride)
+    oracle.render(scene, st, spp, mb, first_frame=1)
+    return img, st
+
+
+def test_config1_01_kat(gpu, oracle):
+    img, st = run_pair(gpu, oracle, scenes.scene_01(), 256, 256, 1, 1)
+    assert np.array_equal(img, st.rgba)
+    cols, counts = np.unique(img.reshape(-1, 4), axis=0, return_counts=True)
+    assert cols.tolist() == [[0, 0, 0, 255], [209, 0, 0, 255]]
+    assert counts.tolist() == [59099, 6437]
+    same_state(gpu, st)
+
+
+@pytest.mark.parametrize("w,h,spp,mb", [(320, 180, 4, 4), (1280, 720, 2, 5)])
+def test_07_small(gpu, oracle, w, h, spp, mb):
+    img, st = run_pair(gpu, oracle, scenes.scene_07(), w, h, spp, mb)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+def test_config3_07_full_size(gpu, oracle):
+    """BASELINE config 3 exactly: 07 scene, 1920x1080, 8 spp, 4 bounces."""
+    img, st = run_pair(gpu, oracle, scenes.scene_07(), 1920, 1080, 8, 4)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+def test_config2_04(gpu, oracle):
+    img, st = run_pair(gpu, oracle, scenes.scene_04(), 1280, 720, 4, 3)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+def test_quads_04_box(gpu, oracle):
+    img, st = run_pair(gpu, oracle, scenes.scene_04_box(), 640, 360, 4, 5)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+def test_stress_scene_small(gpu, oracle):
+    img, st = run_pair(gpu, oracle, scenes.stress_scene(), 96, 54, 2, 8)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+@pytest.mark.parametrize("w,h", [(100, 37), (1, 1), (63, 65)])
+def test_ragged_sizes(gpu, oracle, w, h):
+    img, st = run_pair(gpu, oracle, scenes.scene_07(), w, h, 3, 4)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+@pytest.mark.parametrize("mb", [0, 1, 12, 32])
+def test_bounce_limits(gpu, oracle, mb):
+    img, st = run_pair(gpu, oracle, scenes.scene_07(), 160, 90, 2, mb)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+def test_empty_scene(gpu, oracle):
+    img, st = run_pair(gpu, oracle, scenes.empty_scene(), 128, 72, 2, 4)
+    assert np.array_equal(img, st.rgba)
+    assert (img[..., :3] == 0).all() and (img[..., 3] == 255).all()
+
+
+def test_progressive_continuation(gpu, oracle):
+    """3 frames then 5 more (continuing the frame counter) == 8 frames at once
+    (Main.cu:467-480), and a reset restarts accumulation but not the RNG."""
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    w, h = 256, 144
+    gpu.render(w, h, 3, 4, first_frame=1)
+    assert gpu.frame_counter == 4
+    img = gpu.render(w, h, 5, 4)  # first_frame=0: continue at 4
+    assert gpu.frame_counter == 9
+    st = oracle.OracleState(w, h)
+    oracle.render(s, st, 8, 4, first_frame=1)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+    gpu.reset_accumulation()
+    img2 = gpu.render(w, h, 2, 4)
+    oracle.render(s, st, 2, 4, first_frame=1)
+    assert np.array_equal(img2, st.rgba)
+    same_state(gpu, st)
+
+
+def test_drop_in_render_entry_point(gpu, oracle):
+    """rt_render(ctx, width, height, samples): context max_bounces (default 5)."""
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    gpu.set_max_bounces(5)
+    img = gpu.render_simple(192, 108, 4)
+    st = oracle.OracleState(192, 108)
+    oracle.render(s, st, 4, 5, first_frame=1)
+    assert np.array_equal(img, st.rgba)
+
+
+@pytest.mark.parametrize("stride", [2, 3, 8])
+def test_row_shards_match_full_image(gpu, oracle, stride):
+    """Pixel-row shards (the multi-GPU partition) are byte-identical to the
+    corresponding rows of the full image: the RNG seed is the global index."""
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    w, h = 320, 180
+    full = gpu.render(w, h, 4, 4, first_frame=1)
+    for r in range(stride):
+        part = gpu.render(w, h, 4, 4, first_frame=1, row_offset=r, row_stride=stride)
+        assert np.array_equal(part, full[r::stride])
+
+
+def test_checkpoint_resume(gpu, oracle):
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    w, h = 128, 96
+    gpu.render(w, h, 3, 4, first_frame=1)
+    rng, acc = gpu.get_state(h, w)
+    gpu.render(w, h, 2, 4)                    # advance, then roll back
+    gpu.set_state(rng, acc, 4)
+    img = gpu.render(w, h, 2, 4)
+    st = oracle.OracleState(w, h)
+    oracle.render(s, st, 5, 4, first_frame=1)
+    assert np.array_equal(img, st.rgba)
+
+
+def test_camera_moved(gpu, oracle):
+    """A rotated/moved camera (controls(), Controls.cuh:5-75) resets accumulation."""
+    from bwrt.abi import Camera, Vec3
+    import ctypes as C
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    gpu.render(160, 90, 2, 4, first_frame=1)
+    cam = Camera(Vec3(0.3, 1.2, 0.5), (C.c_float * 2)(0.35, -0.2), s.camera.fov)
+    gpu.set_camera(cam)
+    assert gpu.frame_counter == 1
+    img = gpu.render(160, 90, 2, 4)
+    s.set_camera(cam)
+    # oracle: the same two frames of the original view first (RNG continues)
+    st2 = oracle.OracleState(160, 90)
+    oracle.render(scenes.scene_07(), st2, 2, 4, first_frame=1)
+    oracle.render(s, st2, 2, 4, first_frame=1)
+    assert np.array_equal(img, st2.rgba)
+
+
+def test_converges_to_reference_png(gpu):
+    """Real-CUDA sanity (statistical): 1024 frames of the 07 scene at
+    1920x1080, maxBounces 5 (Main.cu:26) vs Renders/07_specular_BRDF.png:
+    16x16 block-mean MAE <= 1.5 LSB (fixture tests/golden/07_png_blocks16.npz)."""
+    g = np.load(os.path.join(GOLDEN, "07_png_blocks16.npz"))
+    gpu.set_scene(scenes.scene_07())
+    gpu.render(1920, 1080, 512, 5, first_frame=1)
+    img = gpu.render(1920, 1080, 512, 5)
+    top = img[::-1, :, :3]
+    dx, dy, ph, pw, b = (int(g[k]) for k in ("dx", "dy", "png_h", "png_w", "block"))
+    crop = top[dy:dy + ph, dx:dx + pw]
+    hh, ww = ph // b * b, pw // b * b
+    blocks = crop[:hh, :ww].astype(np.float64).reshape(hh // b, b, ww // b, b, 3).mean((1, 3))
+    mae = np.abs(blocks - g["blocks"]).mean()
+    ref = os.path.join(GOLDEN, "oracle_07_1024.json")
+    if os.path.exists(ref):
+        # the GPU is bit-exact with the oracle, so it reproduces the oracle's MAE
+        assert abs(mae - json.load(open(ref))["block_mean_mae_lsb"]) < 1e-6
+    assert mae <= 1.5, mae
