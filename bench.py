@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE.json's headline metric on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): the 07_specular_BRDF
+scene (reference Main.cu:39-67), 1920x1080, 8 spp (= 8 progressive frames,
+accumulatedFrames 1..8), maxBounces 4.  One "step" renders that full 8-spp
+frame from scratch (accumulation reset, RNG streams continuing like the
+reference's controls() reset) with inputs already resident in HBM, and — for
+N > 1 — includes the RCCL gather of the RGBA8 image to rank 0 and the
+de-interleave kernel.  The frame is fixed, so N GPUs split it by interleaved
+pixel rows: strong scaling.
+
+Metric: Msamples/s (nominal) = W*H*spp*bounces / t / 1e6,
+ms/frame = ms_per_step.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+                  [--no-cpu-baseline] [--cpu-threads T]
+For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "bwidman-raytracer_amd")]
+
+import torch  # noqa: E402  (import torch BEFORE libbwrt: one shared HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+from bwrt import Renderer, abi, scenes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BYTES_PER_PIXEL_PASS = 76  # rng 24+24, frameSum 12+12, RGBA8 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(scenes.CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(scene_key, w, h, spp, mb, threads):
+    """The oracle (C restatement, OpenMP over rows) on the host cores: the
+    reported CPU baseline ("port"), never the measured product."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    O.build()
+    if threads <= 0:
+        threads = min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1))
+    scene = scenes.SCENES[scene_key]()
+    st = O.OracleState(w, h)
+    O.render(scene, st, 1, mb, first_frame=1, threads=threads)  # warm (pages, threads)
+    st = O.OracleState(w, h)
+    t0 = time.perf_counter()
+    O.render(scene, st, spp, mb, first_frame=1, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(w * h * spp * mb / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
+            "kind": "port", "ms_per_frame": round(dt * 1e3, 2),
+            "sample": f"one full {w}x{h} {spp}-spp {mb}-bounce frame of scene {scene_key} "
+                      f"(oracle/oracle.c, OpenMP, {threads} threads)"}
+
+
+def load_traffic(path, workload_key):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == workload_key:
+            return t
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    scene_key, W, H, SPP, MB, _ = scenes.CONFIGS[args.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lib = abi.load()
+    hip_libs = sorted({l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l})
+    if len(hip_libs) != 1:
+        print(f"warning: {len(hip_libs)} HIP runtimes loaded: {hip_libs}", file=sys.stderr)
+    r = Renderer(local, lib=lib)
+    scene = scenes.SCENES[scene_key]()
+    r.set_scene(scene)
+    rows_per = (H + world - 1) // world
+    my_rows = lib.rt_shard_rows(H, rank, world)
+    r.init_rand(W, H, rank, world)
+    local_img = torch.zeros(rows_per * W, dtype=torch.int32, device=dev)
+    full_img = torch.empty(H * W, dtype=torch.int32, device=dev) if rank == 0 else None
+    gathered = torch.empty(world * rows_per * W, dtype=torch.int32, device=dev) if world > 1 else None
+    # a dedicated (non-null) stream: the kernel, its timing events and the
+    # RCCL gather are all ordered on it (NULL would mean the context's own
+    # stream in the C ABI)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    params = r.params(W, H, SPP, MB, first_frame=1, row_offset=rank, row_stride=world)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        r.render_device(params, local_img.data_ptr() if world > 1 else full_img.data_ptr(),
+                        stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local_img)
+            if rank == 0:
+                r.deinterleave_device(gathered.data_ptr(), full_img.data_ptr(), W, H, world, rows_per,
+                                      stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in events]
+    t = torch.tensor([elapsed, sum(kern_ms) / len(kern_ms)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_avg_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        samples = W * H * SPP * MB * args.steps
+        value = samples / elapsed / 1e6
+        # roofline of the dominant kernel (rt_render_kernel), per launch
+        units = my_rows * W * SPP  # pixel-passes in one launch on this rank
+        alg_bytes = units * BYTES_PER_PIXEL_PASS
+        achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
+        workload_key = f"{scene_key}-{W}x{H}-{SPP}spp-{MB}b-rows{world}"
+        traffic = load_traffic(args.traffic_json, workload_key)
+        out = {
+            "metric": "Msamples/sec (W*H*spp*bounces/t), 1920x1080 8spp 4-bounce, 07_specular_BRDF",
+            "value": round(value, 2),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference scene 07 (Main.cu:39-67), per-pixel RNG seeded y*W+x",
+            "config": {"workload": f"07_specular_BRDF {W}x{H} {SPP}spp {MB}-bounce (BASELINE configs[2])"
+                       if args.config == "c3" else f"{args.config}: scene {scene_key} {W}x{H} {SPP}spp {MB}-bounce",
+                       "scene": scene_key, "width": W, "height": H, "spp": SPP, "max_bounces": MB,
+                       "parallelism": f"pixel-rows/{world}" + (" + rccl all_gather" if world > 1 else "")},
+            "ms_per_frame": round(ms_step, 4),
+            "kernel_ms_avg": round(kern_avg_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": (round(traffic["hbm_bytes_per_launch"]) if traffic else None),
+                         "kernel": "rt_render_kernel",
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "bytes_per_unit": BYTES_PER_PIXEL_PASS, "units_per_launch": units},
+        }
+        if traffic and traffic.get("valu"):
+            out["valu"] = traffic["valu"]
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene_key, W, H, SPP, MB, args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

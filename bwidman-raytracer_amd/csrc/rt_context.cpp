@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -21,7 +22,7 @@
 #include "../../include/rt_abi.h"
 #include "rt_layout.h"
 
-hipError_t rt_launch_render(const rt_kparams& K, int block, hipStream_t stream);
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, hipStream_t stream);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
                                hipStream_t stream);
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
@@ -64,6 +65,8 @@ struct DevBuf {
 
 struct rt_context {
     int device = 0;
+    int num_cus = 256;
+    int grid_mult = 0;  // persistent grid = grid_mult x resident workgroups per CU x CUs
     hipStream_t stream = nullptr;
     hipStream_t last_stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -137,7 +140,7 @@ void put_material(float* h, const rt_material& m) {
     h[8] = m.roughness;
     // fresnel(): square(ior)/square(1.0f) - 1.0f (Main.cu:125)
     h[9] = (m.refractive_index * m.refractive_index) / (1.0f * 1.0f) - 1.0f;
-    h[10] = 0.0f;
+    h[10] = m.roughness * m.roughness;  // Main.cu:119 evaluates roughness*roughness first
     h[11] = 0.0f;
 }
 
@@ -204,6 +207,10 @@ int rt_create(int device, rt_context** out) {
         return RT_ERR_HIP;
     }
     c->last_stream = c->stream;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->num_cus = prop.multiProcessorCount;
+    if (const char* gm = std::getenv("BWRT_GRID_MULT")) c->grid_mult = std::atoi(gm);
     *out = c;
     return RT_OK;
 }
@@ -415,9 +422,8 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
 }
 
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
-    const int block = (K.max_bounces + 1) * 7 * 256 * 4 <= 65536 ? 256 : 64;
     HIP_TRY(c, hipEventRecord(c->ev0, s));
-    hipError_t e = rt_launch_render(K, block, s);
+    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, s);
     if (e != hipSuccess) return hip_fail(c, e, "rt_render_kernel launch");
     HIP_TRY(c, hipEventRecord(c->ev1, s));
     c->timed = true;

@@ -79,9 +79,11 @@ __device__ __forceinline__ unsigned next_u32(Xorwow& s) {
 }
 
 // Math.cuh:277-279: float(u)/INT_MAX*0.5f*max, INT_MAX -> 2^31 exactly
+// Every step after the u32 -> float rounding is an exact power-of-two
+// scaling, so the value equals u * (2^-32 * max) with max in {1, 2}.
 __device__ __forceinline__ float rand_range(Xorwow& s, float max) {
     float u = (float)next_u32(s);
-    return ((u / 2147483648.0f) * 0.5f) * max;
+    return u * (2.3283064365386963e-10f * max);
 }
 
 // ---- transcendentals: the exact operation sequence of oracle.c
@@ -179,11 +181,12 @@ __device__ __forceinline__ float atan_nn(float x) {  // orc_atanf
 }
 
 // ---- BRDF helpers (Main.cu:111-206)
-__device__ __forceinline__ float shadowing_masking(f3 dir, f3 n, f3 m, float rough) {
+// rough2 = roughness * roughness (precomputed: the reference evaluates
+// roughness * roughness * tanTheta * tanTheta left to right, Main.cu:119)
+__device__ __forceinline__ float shadowing_masking(f3 dir, f3 n, f3 m, float rough2) {
     float vdn = dot(dir, n);
     float tan_theta = fmaxf(1.0f / (vdn * vdn) - 1.0f, 0.0f);
-    return chi(dot(dir, m) / vdn) * 2.0f /
-           (1.0f + sqrtf(1.0f + rough * rough * tan_theta * tan_theta));
+    return chi(dot(dir, m) / vdn) * 2.0f / (1.0f + sqrtf(1.0f + rough2 * tan_theta * tan_theta));
 }
 
 // fresnel(i, m, 1, ior) with ior2m1 = ior*ior/(1*1) - 1 precomputed
@@ -196,8 +199,8 @@ __device__ __forceinline__ float fresnel(f3 incident, f3 normal, float ior2m1) {
            (1.0f + square(c * (g + c) - 1.0f) / square(c * (g - c) + 1.0f));
 }
 
-__device__ __forceinline__ float specular_weight(f3 i, f3 o, f3 n, f3 m, float rough) {
-    float g = shadowing_masking(i, n, m, rough) * shadowing_masking(o, n, m, rough);
+__device__ __forceinline__ float specular_weight(f3 i, f3 o, f3 n, f3 m, float rough2) {
+    float g = shadowing_masking(i, n, m, rough2) * shadowing_masking(o, n, m, rough2);
     if (isnan(g)) return 1.0f;
     float den = fabsf(dot(i, n) * dot(m, n));
     if (den == 0.0f) den = RT_NEAR_ZERO;
@@ -213,7 +216,10 @@ __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal) {
         float y = rand_range(s, 2.0f) - 1.0f;
         float z = rand_range(s, 2.0f) - 1.0f;
         r = mk(x, y, z);
-    } while (length3(r) > 1.0f);
+        // length(r) > 1 (Main.cu:197) <=> RN(x*x+y*y+z*z) > 1 + 2^-23: sqrt is
+        // correctly rounded, so RN(sqrt(s)) > 1 iff s >= 1 + 2^-22 (checked
+        // exhaustively in tests/test_numerics.py)
+    } while (r.x * r.x + r.y * r.y + r.z * r.z > 1.00000012f);
     r = normalize3(r);
     if (dot(normal, r) < 0.0f) r = sub(r, scale(2.0f * dot(r, normal), normal));
     return r;
@@ -274,7 +280,9 @@ __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, flo
             float b = 2.0f * dot(xp, d);
             float c = dot(xp, xp) - s[3];
             float disc = b * b - a4 * c;
-            if (!(disc < 0.0f)) {
+            // exact early-out: b >= 0 (finite disc, a2 > 0) gives -b - sqrt(disc) <= 0,
+            // i.e. t <= 0 <= nearZero, rejected by the reference as well
+            if (!(disc < 0.0f) && !(b >= 0.0f && disc == disc && a2 > 0.0f)) {
                 float t = (-b - sqrtf(disc)) / a2;
                 if (!(t <= RT_NEAR_ZERO || t > best_t)) {
                     best_t = t;
@@ -299,18 +307,6 @@ __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, flo
     }
 }
 
-// LDS record stack: rec[(level*7 + field) * blockDim + lane]
-__device__ __forceinline__ void push_record(float* rec, int stride, int lvl, f3 e, f3 b, float c) {
-    float* r = rec + (lvl * 7) * stride;
-    r[0 * stride] = e.x;
-    r[1 * stride] = e.y;
-    r[2 * stride] = e.z;
-    r[3 * stride] = b.x;
-    r[4 * stride] = b.y;
-    r[5 * stride] = b.z;
-    r[6 * stride] = c;
-}
-
 __device__ __forceinline__ unsigned to_u8(float v) {
     float r = roundf(v);
     if (r != r) return 0u;  // NaN -> 0
@@ -319,169 +315,225 @@ __device__ __forceinline__ unsigned to_u8(float v) {
     return (unsigned)r;
 }
 
+// Main.cu:305-312: frameSum / n -> ACES (Math.cuh:253-262) -> gamma
+// (Math.cuh:249-251) -> *255 -> round -> uchar4(r, g, b, 255)
+__device__ __forceinline__ unsigned tone_map(float ax, float ay, float az, unsigned n) {
+    const float inv = 1.0f / (float)n;
+    float v[3] = {inv * ax, inv * ay, inv * az};
+    unsigned px = 0xff000000u;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        float cc = 0.6f * v[ch];  // color *= 0.6
+        float num = cc * (2.51f * cc + 0.03f);
+        float den = cc * (2.43f * cc + 0.59f) + 0.14f;
+        float tm = fminf(num / den, 1.0f);  // clamp(color, 1.0f): upper only
+        float g = sqrtf(tm) * 255.0f;
+        px |= to_u8(g) << (8 * ch);
+    }
+    return px;
+}
+
+// Per-lane pixel state ------------------------------------------------------
+struct PixelState {
+    long p;         // shard pixel index
+    bool valid;
+    Xorwow rs;
+    float ax, ay, az;  // frameSum
+    f3 d0;          // normalize(rot * pixelPosition): the same every frame
+    int passes_left;
+    unsigned frame;
+};
+
+__device__ __forceinline__ void load_pixel(const rt_kparams& K, long npix, long p, PixelState& s) {
+    s.p = p;
+    s.valid = p < npix;
+    s.passes_left = 0;
+    s.frame = K.first_frame;
+    if (!s.valid) return;
+    const int j = (int)(p / K.width);
+    const int x = (int)(p - (long)j * K.width);
+    const int y = K.row_offset + j * K.row_stride;
+    s.rs.d = K.rng[0 * npix + p];
+    s.rs.v0 = K.rng[1 * npix + p];
+    s.rs.v1 = K.rng[2 * npix + p];
+    s.rs.v2 = K.rng[3 * npix + p];
+    s.rs.v3 = K.rng[4 * npix + p];
+    s.rs.v4 = K.rng[5 * npix + p];
+    s.ax = s.ay = s.az = 0.0f;
+    if (K.first_frame != 1u) {
+        s.ax = K.accum[0 * npix + p];
+        s.ay = K.accum[1 * npix + p];
+        s.az = K.accum[2 * npix + p];
+    }
+    // Main.cu:287-290: pixelPosition, rotLeft*rotUp*pixelPosition, normalize
+    const f3 pix = mk((float)(x - K.width / 2), (float)(y - K.height / 2), K.screen_z);
+    const f3 pr = mk(K.rot[0] * pix.x + K.rot[1] * pix.y + K.rot[2] * pix.z,
+                     K.rot[3] * pix.x + K.rot[4] * pix.y + K.rot[5] * pix.z,
+                     K.rot[6] * pix.x + K.rot[7] * pix.y + K.rot[8] * pix.z);
+    s.d0 = normalize3(pr);
+    s.passes_left = K.samples;
+}
+
+__device__ __forceinline__ void store_pixel(const rt_kparams& K, long npix, const PixelState& s) {
+    const long p = s.p;
+    K.rng[0 * npix + p] = s.rs.d;
+    K.rng[1 * npix + p] = s.rs.v0;
+    K.rng[2 * npix + p] = s.rs.v1;
+    K.rng[3 * npix + p] = s.rs.v2;
+    K.rng[4 * npix + p] = s.rs.v3;
+    K.rng[5 * npix + p] = s.rs.v4;
+    K.accum[0 * npix + p] = s.ax;
+    K.accum[1 * npix + p] = s.ay;
+    K.accum[2 * npix + p] = s.az;
+    if (K.rgba) K.rgba[p] = tone_map(s.ax, s.ay, s.az, s.frame - 1u);
+}
+
 }  // namespace
 
-// One thread = one pixel of the shard; all K.samples frames in one launch.
-__global__ void __launch_bounds__(256) rt_render_kernel(rt_kparams K) {
-    extern __shared__ float rec_lds[];
-    const int stride = blockDim.x;
-    float* rec = rec_lds + threadIdx.x;
+// LDS layout: [hit table, n_prim*12 floats, if HIT_LDS] then the record stack
+// of the recursion, 3 dwords per level per lane, lane-minor:
+//   code[l][lane] (int: primitive id, ~id for a specular bounce),
+//   kspec[l][lane] (specular brdf scalar), cosang[l][lane]
+// (bank = lane: conflict-free for any per-lane depth).
+//
+// Persistent lanes: the grid covers the GPU once (occupancy-sized); lane g
+// renders pixels g, g+T, g+2T, ... (T = lanes in the grid), each for all
+// K.samples frames, regenerating its next path in the iteration after the
+// previous one ends.  A wave ends when all its lanes ran out of pixels.
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 1
+#endif
+
+template <int BLOCK, bool HIT_LDS>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
+rt_render_kernel(rt_kparams K) {
+    extern __shared__ float smem[];
+    const int tid = threadIdx.x;
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    const float* hit_tab = K.hit;
+    float* rec_base = smem;
+    if (HIT_LDS) {
+        for (int i = tid; i < n_prim * RT_HIT_FLOATS; i += BLOCK) smem[i] = K.hit[i];
+        __syncthreads();
+        hit_tab = smem;
+        rec_base = smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3);
+    }
+    int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
+    float* rec_k = rec_base + (K.max_bounces + 1) * BLOCK + tid;
+    float* rec_c = rec_base + 2 * (K.max_bounces + 1) * BLOCK + tid;
 
     const long npix = (long)K.rows * K.width;
-    const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = p < npix;
-
-    int x = 0, y = 0;
-    Xorwow rs = {0, 0, 0, 0, 0, 0};
-    float accx = 0.0f, accy = 0.0f, accz = 0.0f;
-    int passes_left = 0;
-    if (valid) {
-        const int j = (int)(p / K.width);
-        x = (int)(p - (long)j * K.width);
-        y = K.row_offset + j * K.row_stride;
-        rs.d = K.rng[0 * npix + p];
-        rs.v0 = K.rng[1 * npix + p];
-        rs.v1 = K.rng[2 * npix + p];
-        rs.v2 = K.rng[3 * npix + p];
-        rs.v3 = K.rng[4 * npix + p];
-        rs.v4 = K.rng[5 * npix + p];
-        if (K.first_frame != 1u) {
-            accx = K.accum[0 * npix + p];
-            accy = K.accum[1 * npix + p];
-            accz = K.accum[2 * npix + p];
-        }
-        passes_left = K.samples;
-    }
-    unsigned frame = K.first_frame;
+    const long T = (long)gridDim.x * BLOCK;
+    PixelState px;
+    load_pixel(K, npix, (long)blockIdx.x * BLOCK + tid, px);
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     int depth = -1;  // -1: needs a camera ray for its next frame
-
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
-    const f3 pix0 = mk((float)(x - K.width / 2), (float)(y - K.height / 2), K.screen_z);
 
     while (true) {
-        // (1) regenerate: camera ray + anti-aliasing jitter (Main.cu:287-292)
-        if (depth < 0 && passes_left > 0) {
-            f3 pr = mk(K.rot[0] * pix0.x + K.rot[1] * pix0.y + K.rot[2] * pix0.z,
-                       K.rot[3] * pix0.x + K.rot[4] * pix0.y + K.rot[5] * pix0.z,
-                       K.rot[6] * pix0.x + K.rot[7] * pix0.y + K.rot[8] * pix0.z);
-            d = normalize3(pr);
-            f3 jit = random_direction(rs, d);
-            d = add(d, scale(K.jitter, jit));
-            d = normalize3(d);
+        // (1) regenerate: jittered camera ray (Main.cu:290-292)
+        if (depth < 0 && px.passes_left > 0) {
+            f3 jit = random_direction(px.rs, px.d0);
+            d = normalize3(add(px.d0, scale(K.jitter, jit)));
             o = cam;
             depth = 0;
         }
         const bool active = depth >= 0;
         if (__ballot(active) == 0ull) break;
-        if (!active) continue;
+        if (active) {
+            // (2) closest hit (Main.cu:214-234)
+            float t;
+            int id;
+            closest_hit(K, o, d, t, id);
 
-        // (2) closest hit (Main.cu:214-234)
-        float t;
-        int id;
-        closest_hit(K, o, d, t, id);
+            bool finished = true;
+            if (id >= 0) {
+                // (3) shade (Main.cu:237-264)
+                const float* h = hit_tab + RT_HIT_FLOATS * id;
+                const float4 h0 = *reinterpret_cast<const float4*>(h);
+                const float4 h1 = *reinterpret_cast<const float4*>(h + 4);
+                const float4 h2 = *reinterpret_cast<const float4*>(h + 8);
+                const f3 P = add(o, scale(t, d));
+                f3 n = mk(h0.x, h0.y, h0.z);
+                if (h0.w != 0.0f) n = normalize3(sub(P, n));  // sphere: centre -> normal
+                const f3 albedo = mk(h1.x, h1.y, h1.z);
+                const float rough = h2.x, ior2m1 = h2.y, rough2 = h2.z;
 
-        bool finished = true;
-        if (id >= 0) {
-            // (3) shade (Main.cu:237-264)
-            const float* h = K.hit + RT_HIT_FLOATS * id;
-            const float4 h0 = *reinterpret_cast<const float4*>(h);
-            const float4 h1 = *reinterpret_cast<const float4*>(h + 4);
-            const float4 h2 = *reinterpret_cast<const float4*>(h + 8);
-            const f3 P = add(o, scale(t, d));
-            f3 n = mk(h0.x, h0.y, h0.z);
-            if (h0.w != 0.0f) n = normalize3(sub(P, n));  // sphere: centre -> normal
-            const f3 albedo = mk(h1.x, h1.y, h1.z);
-            const float emittance = h1.w, rough = h2.x, ior2m1 = h2.y;
-            const f3 e = scale(emittance, albedo);
-
-            f3 scatter, b;
-            const float choice = rand_range(rs, 1.0f);
-            if (choice < RT_SPECULAR_CHANCE) {
-                // genMicrofacetNormal (Main.cu:170-185)
-                const float e1 = rand_range(rs, 1.0f);
-                const float e2 = rand_range(rs, 1.0f);
-                const float theta = atan_nn(rough * sqrtf(e1) / sqrtf(1.0f - e1));
-                const float phi = 2.0f * RT_PI * e2;
-                float st, ct, sp, cp;
-                sincos_nn(theta, st, ct);
-                sincos_nn(phi, sp, cp);
-                const f3 mloc = mk(st * cp, st * sp, ct);
-                // baseAroundNormalToRegular (Main.cu:149-168)
-                f3 some = mk(1.0f, 0.0f, 0.0f);
-                if (fabsf(dot(n, some)) < 1.0f - RT_NEAR_ZERO) some = mk(0.0f, 1.0f, 0.0f);
-                const f3 t1 = cross(n, some);
-                const f3 t2 = cross(n, t1);
-                const f3 m = mk(dot(mk(t1.x, t2.x, n.x), mloc), dot(mk(t1.y, t2.y, n.y), mloc),
-                                dot(mk(t1.z, t2.z, n.z), mloc));
-                scatter = sub(d, scale(2.0f * dot(d, m), m));  // reflect, Main.cu:187-191
-                const f3 inc = scale(-1.0f, d);
-                const float fr = fresnel(inc, m, ior2m1);
-                const float sw = specular_weight(inc, scatter, n, m, rough);
-                const float k = sw * fr / RT_SPECULAR_CHANCE;
-                b = mk(k, k, k);
-            } else {
-                scatter = random_direction(rs, n);
-                b = scale((float)(2.0 / (1 - RT_SPECULAR_CHANCE)), albedo);
+                f3 scatter;
+                int code = id;
+                float kspec = 0.0f;
+                const float choice = rand_range(px.rs, 1.0f);
+                if (choice < RT_SPECULAR_CHANCE) {
+                    // genMicrofacetNormal (Main.cu:170-185)
+                    const float e1 = rand_range(px.rs, 1.0f);
+                    const float e2 = rand_range(px.rs, 1.0f);
+                    const float theta = atan_nn(rough * sqrtf(e1) / sqrtf(1.0f - e1));
+                    const float phi = 2.0f * RT_PI * e2;
+                    float st, ct, sp, cp;
+                    sincos_nn(theta, st, ct);
+                    sincos_nn(phi, sp, cp);
+                    const f3 mloc = mk(st * cp, st * sp, ct);
+                    // baseAroundNormalToRegular (Main.cu:149-168)
+                    f3 some = mk(1.0f, 0.0f, 0.0f);
+                    if (fabsf(dot(n, some)) < 1.0f - RT_NEAR_ZERO) some = mk(0.0f, 1.0f, 0.0f);
+                    const f3 t1 = cross(n, some);
+                    const f3 t2 = cross(n, t1);
+                    const f3 m = mk(dot(mk(t1.x, t2.x, n.x), mloc), dot(mk(t1.y, t2.y, n.y), mloc),
+                                    dot(mk(t1.z, t2.z, n.z), mloc));
+                    scatter = sub(d, scale(2.0f * dot(d, m), m));  // reflect, Main.cu:187-191
+                    const f3 inc = scale(-1.0f, d);
+                    const float fr = fresnel(inc, m, ior2m1);
+                    const float sw = specular_weight(inc, scatter, n, m, rough2);
+                    kspec = sw * fr / RT_SPECULAR_CHANCE;  // brdf = (s*F/0.5) * {1,1,1}
+                    code = ~id;
+                } else {
+                    scatter = random_direction(px.rs, n);  // brdf = 4 * albedo
+                }
+                (void)albedo;
+                rec_code[depth * BLOCK] = code;
+                rec_k[depth * BLOCK] = kspec;
+                rec_c[depth * BLOCK] = dot(scatter, n);  // cosAngle, Main.cu:264
+                depth++;
+                o = P;
+                d = scatter;
+                finished = depth > K.max_bounces;  // Main.cu:210
             }
-            const float c = dot(scatter, n);
-            push_record(rec, stride, depth, e, b, c);
-            depth++;
-            o = P;
-            d = scatter;
-            finished = depth > K.max_bounces;  // Main.cu:210
-        }
-        if (finished) {
-            // (4) fold the recursion innermost-first (Main.cu:262-268)
-            float lx = 0.0f, ly = 0.0f, lz = 0.0f;  // backgroundColor
-            for (int l = depth - 1; l >= 0; --l) {
-                const float* r = rec + (l * 7) * stride;
-                const float c = r[6 * stride];
-                lx = r[0 * stride] + (r[3 * stride] * lx) * c;
-                ly = r[1 * stride] + (r[4 * stride] * ly) * c;
-                lz = r[2 * stride] + (r[5 * stride] * lz) * c;
+            if (finished) {
+                // (4) fold the recursion innermost-first (Main.cu:262-268):
+                //     L = emitted + (brdf * L) * cosAngle
+                float lx = 0.0f, ly = 0.0f, lz = 0.0f;  // backgroundColor
+                for (int l = depth - 1; l >= 0; --l) {
+                    const int c0 = rec_code[l * BLOCK];
+                    const float k = rec_k[l * BLOCK];
+                    const float c = rec_c[l * BLOCK];
+                    const bool spec = c0 < 0;
+                    const float4 mat = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * (spec ? ~c0 : c0) + 4);
+                    const float ex = mat.w * mat.x, ey = mat.w * mat.y, ez = mat.w * mat.z;  // emittance * albedo
+                    const float dk = (float)(2.0 / (1 - RT_SPECULAR_CHANCE));                 // 4.0f
+                    const float bx = spec ? k : dk * mat.x, by = spec ? k : dk * mat.y, bz = spec ? k : dk * mat.z;
+                    lx = ex + (bx * lx) * c;
+                    ly = ey + (by * ly) * c;
+                    lz = ez + (bz * lz) * c;
+                }
+                // (5) progressive accumulation (Main.cu:299-304), spp = 1
+                if (px.frame == 1u) {
+                    px.ax = 0.0f;
+                    px.ay = 0.0f;
+                    px.az = 0.0f;
+                }
+                px.ax = px.ax + lx;
+                px.ay = px.ay + ly;
+                px.az = px.az + lz;
+                px.frame++;
+                px.passes_left--;
+                depth = -1;
+                if (px.passes_left == 0) {  // pixel done: write back, take the next one
+                    store_pixel(K, npix, px);
+                    load_pixel(K, npix, px.p + T, px);
+                }
             }
-            // (5) progressive accumulation (Main.cu:299-304), spp = 1
-            if (frame == 1u) {
-                accx = 0.0f;
-                accy = 0.0f;
-                accz = 0.0f;
-            }
-            accx = accx + lx;
-            accy = accy + ly;
-            accz = accz + lz;
-            frame++;
-            passes_left--;
-            depth = -1;
         }
-    }
-
-    if (!valid) return;
-    K.rng[0 * npix + p] = rs.d;
-    K.rng[1 * npix + p] = rs.v0;
-    K.rng[2 * npix + p] = rs.v1;
-    K.rng[3 * npix + p] = rs.v2;
-    K.rng[4 * npix + p] = rs.v3;
-    K.rng[5 * npix + p] = rs.v4;
-    K.accum[0 * npix + p] = accx;
-    K.accum[1 * npix + p] = accy;
-    K.accum[2 * npix + p] = accz;
-    if (K.rgba) {
-        // Main.cu:305-312: frameSum / n -> ACES -> gamma -> *255 -> round
-        const float inv = 1.0f / (float)(frame - 1u);
-        float v[3] = {inv * accx, inv * accy, inv * accz};
-        unsigned px = 0xff000000u;
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) {
-            float cc = 0.6f * v[ch];  // Math.cuh:255, color *= 0.6
-            float num = cc * (2.51f * cc + 0.03f);
-            float den = cc * (2.43f * cc + 0.59f) + 0.14f;
-            float tm = fminf(num / den, 1.0f);
-            float g = sqrtf(tm) * 255.0f;  // gammaCorrection, *= 255
-            px |= to_u8(g) << (8 * ch);
-        }
-        K.rgba[p] = px;
     }
 }
 
@@ -522,12 +574,54 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 }
 
 // ---- launchers (host side) ------------------------------------------------
-hipError_t rt_launch_render(const rt_kparams& K, int block, hipStream_t stream) {
+namespace {
+template <int BLOCK, bool HIT_LDS>
+hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_cap, hipStream_t stream) {
     const long npix = (long)K.rows * K.width;
-    const unsigned grid = (unsigned)((npix + block - 1) / block);
-    const size_t lds = (size_t)(K.max_bounces + 1) * 7 * block * sizeof(float);
-    hipLaunchKernelGGL(rt_render_kernel, dim3(grid), dim3(block), lds, stream, K);
+    long grid = (npix + BLOCK - 1) / BLOCK;
+    if (grid_cap > 0 && grid > grid_cap) grid = grid_cap;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
     return hipGetLastError();
+}
+
+template <int BLOCK, bool HIT_LDS>
+int resident_blocks_per_cu(size_t lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_render_kernel<BLOCK, HIT_LDS>, BLOCK, lds) != hipSuccess)
+        return 0;
+    return n;
+}
+}  // namespace
+
+// LDS bytes of one workgroup: hit table (if staged) + 3 record dwords per
+// level per lane.
+size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds) {
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
+    return hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
+}
+
+// Host-side launch policy: 256-lane workgroups (64 for very deep paths),
+// hit table in LDS when it fits in 16 KB, persistent grid of
+// waves_per_cu-many resident workgroups per CU (0 = one per 256 pixels).
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, hipStream_t stream) {
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    const bool hit_lds = (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
+    const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 32768;
+    const int block = small_block ? 64 : 256;
+    const size_t lds = rt_render_lds_bytes(K, block, hit_lds);
+    int per_cu = 0;
+    if (grid_mult > 0) {
+        if (small_block)
+            per_cu = hit_lds ? resident_blocks_per_cu<64, true>(lds) : resident_blocks_per_cu<64, false>(lds);
+        else
+            per_cu = hit_lds ? resident_blocks_per_cu<256, true>(lds) : resident_blocks_per_cu<256, false>(lds);
+    }
+    const int cap = (grid_mult > 0 && per_cu > 0) ? per_cu * num_cus * grid_mult : 0;
+    if (small_block)
+        return hit_lds ? launch_render<64, true>(K, lds, cap, stream) : launch_render<64, false>(K, lds, cap, stream);
+    return hit_lds ? launch_render<256, true>(K, lds, cap, stream) : launch_render<256, false>(K, lds, cap, stream);
 }
 
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,

@@ -29,6 +29,7 @@ def same_state(gpu, st_oracle):
 
 def run_pair(gpu, oracle, scene, w, h, spp, mb, row_offset=0, row_stride=1):
     gpu.set_scene(scene)
+    gpu.init_rand(w, h, row_offset, row_stride)  # reseed: RNG streams persist across renders
     img = gpu.render(w, h, spp, mb, first_frame=1, row_offset=row_offset, row_stride=row_stride)
     st = oracle.OracleState(w, h, row_offset, row_stride)
     oracle.render(scene, st, spp, mb, first_frame=1)
@@ -102,6 +103,7 @@ def test_progressive_continuation(gpu, oracle):
     s = scenes.scene_07()
     gpu.set_scene(s)
     w, h = 256, 144
+    gpu.init_rand(w, h)
     gpu.render(w, h, 3, 4, first_frame=1)
     assert gpu.frame_counter == 4
     img = gpu.render(w, h, 5, 4)  # first_frame=0: continue at 4
@@ -122,6 +124,7 @@ def test_drop_in_render_entry_point(gpu, oracle):
     s = scenes.scene_07()
     gpu.set_scene(s)
     gpu.set_max_bounces(5)
+    gpu.init_rand(192, 108)
     img = gpu.render_simple(192, 108, 4)
     st = oracle.OracleState(192, 108)
     oracle.render(s, st, 4, 5, first_frame=1)
@@ -135,6 +138,7 @@ def test_row_shards_match_full_image(gpu, oracle, stride):
     s = scenes.scene_07()
     gpu.set_scene(s)
     w, h = 320, 180
+    gpu.init_rand(w, h)
     full = gpu.render(w, h, 4, 4, first_frame=1)
     for r in range(stride):
         part = gpu.render(w, h, 4, 4, first_frame=1, row_offset=r, row_stride=stride)
@@ -145,6 +149,7 @@ def test_checkpoint_resume(gpu, oracle):
     s = scenes.scene_07()
     gpu.set_scene(s)
     w, h = 128, 96
+    gpu.init_rand(w, h)
     gpu.render(w, h, 3, 4, first_frame=1)
     rng, acc = gpu.get_state(h, w)
     gpu.render(w, h, 2, 4)                    # advance, then roll back
@@ -161,6 +166,7 @@ def test_camera_moved(gpu, oracle):
     import ctypes as C
     s = scenes.scene_07()
     gpu.set_scene(s)
+    gpu.init_rand(160, 90)
     gpu.render(160, 90, 2, 4, first_frame=1)
     cam = Camera(Vec3(0.3, 1.2, 0.5), (C.c_float * 2)(0.35, -0.2), s.camera.fov)
     gpu.set_camera(cam)
@@ -180,6 +186,7 @@ def test_converges_to_reference_png(gpu):
     16x16 block-mean MAE <= 1.5 LSB (fixture tests/golden/07_png_blocks16.npz)."""
     g = np.load(os.path.join(GOLDEN, "07_png_blocks16.npz"))
     gpu.set_scene(scenes.scene_07())
+    gpu.init_rand(1920, 1080)
     gpu.render(1920, 1080, 512, 5, first_frame=1)
     img = gpu.render(1920, 1080, 512, 5)
     top = img[::-1, :, :3]
