@@ -32,6 +32,7 @@ import torch  # noqa: E402  (import torch BEFORE libbwrt: one shared HIP runtime
 import torch.distributed as dist  # noqa: E402
 
 from bwrt import Renderer, abi, scenes  # noqa: E402
+from bwrt.dist import ShardPlan, gather_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_PIXEL_PASS = 76  # rng 24+24, frameSum 12+12, RGBA8 4
@@ -101,18 +102,20 @@ def main():
     r = Renderer(local, lib=lib)
     scene = scenes.SCENES[scene_key]()
     r.set_scene(scene)
-    rows_per = (H + world - 1) // world
-    my_rows = lib.rt_shard_rows(H, rank, world)
-    r.init_rand(W, H, rank, world)
+    plan = ShardPlan(H, world, rank)
+    rows_per = plan.rows_per_shard
+    my_rows = lib.rt_shard_rows(H, plan.row_offset, plan.row_stride)
+    assert my_rows == plan.rows
+    r.init_rand(W, H, plan.row_offset, plan.row_stride)
     local_img = torch.zeros(rows_per * W, dtype=torch.int32, device=dev)
     full_img = torch.empty(H * W, dtype=torch.int32, device=dev) if rank == 0 else None
-    gathered = torch.empty(world * rows_per * W, dtype=torch.int32, device=dev) if world > 1 else None
+    gathered = torch.empty((world, rows_per * W), dtype=torch.int32, device=dev) if world > 1 else None
     # a dedicated (non-null) stream: the kernel, its timing events and the
     # RCCL gather are all ordered on it (NULL would mean the context's own
     # stream in the C ABI)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    params = r.params(W, H, SPP, MB, first_frame=1, row_offset=rank, row_stride=world)
+    params = r.params(W, H, SPP, MB, first_frame=1, row_offset=plan.row_offset, row_stride=plan.row_stride)
 
     def step(ev=None):
         if ev is not None:
@@ -122,7 +125,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, local_img)
+            gather_rows(local_img, plan, out=gathered)
             if rank == 0:
                 r.deinterleave_device(gathered.data_ptr(), full_img.data_ptr(), W, H, world, rows_per,
                                       stream.cuda_stream)
@@ -184,7 +187,19 @@ def main():
                          "bytes_per_unit": BYTES_PER_PIXEL_PASS, "units_per_launch": units},
         }
         if traffic and traffic.get("valu"):
-            out["valu"] = traffic["valu"]
+            # the binding roofline of this branchy fp32 path: VALU issue.
+            # peak: 256 CUs x 4 SIMD x 64 lanes / 2 cycles x 2.4 GHz
+            v = traffic["valu"]
+            ks = kern_avg_ms * 1e-3
+            lane_peak = 256 * 4 * 64 / 2 * 2.4e9
+            inst_peak = 256 * 4 / 2 * 2.4e9
+            out["valu_roofline"] = {
+                "bound": "valu", "unit": "lane-ops/s", "peak": lane_peak,
+                "achieved": round(v["lane_ops_per_launch"] / ks, 1),
+                "frac": round(v["lane_ops_per_launch"] / ks / lane_peak, 4),
+                "issue_frac": round(v["insts_valu_per_launch"] / ks / inst_peak, 4),
+                "active_lanes_per_valu": round(v["active_lanes_per_valu"], 2),
+                "counters": traffic.get("source")}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene_key, W, H, SPP, MB, args.cpu_threads)
         print(json.dumps(out), flush=True)

@@ -22,7 +22,7 @@
 #include "../../include/rt_abi.h"
 #include "rt_layout.h"
 
-hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, hipStream_t stream);
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, hipStream_t stream);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
                                hipStream_t stream);
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
@@ -66,6 +66,7 @@ struct DevBuf {
 struct rt_context {
     int device = 0;
     int num_cus = 256;
+    bool simple = false;  // BWRT_KERNEL=simple: one-path-per-lane kernel (A/B reference)
     int grid_mult = 0;  // persistent grid = grid_mult x resident workgroups per CU x CUs
     hipStream_t stream = nullptr;
     hipStream_t last_stream = nullptr;
@@ -211,6 +212,7 @@ int rt_create(int device, rt_context** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = prop.multiProcessorCount;
     if (const char* gm = std::getenv("BWRT_GRID_MULT")) c->grid_mult = std::atoi(gm);
+    if (const char* kk = std::getenv("BWRT_KERNEL")) c->simple = std::strcmp(kk, "simple") == 0;
     *out = c;
     return RT_OK;
 }
@@ -422,8 +424,22 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
 }
 
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
+    unsigned long long* stamps = nullptr;
+    if (std::getenv("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS): per-phase wave-cycle sums
+        if (hipMalloc(&stamps, 8 * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemsetAsync(stamps, 0, 8 * sizeof(unsigned long long), s);
+        K.stamps = stamps;
+    }
     HIP_TRY(c, hipEventRecord(c->ev0, s));
-    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, s);
+    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, s);
+    if (stamps) {
+        unsigned long long h[8] = {0};
+        (void)hipMemcpyAsync(h, stamps, sizeof h, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        std::fprintf(stderr, "stamps %llu %llu %llu %llu %llu %llu %llu %llu\n", h[0], h[1], h[2], h[3], h[4], h[5],
+                     h[6], h[7]);
+        (void)hipFree(stamps);
+    }
     if (e != hipSuccess) return hip_fail(c, e, "rt_render_kernel launch");
     HIP_TRY(c, hipEventRecord(c->ev1, s));
     c->timed = true;

@@ -230,7 +230,7 @@ __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal) {
 // (t, primitive id) of the running closest hit are tracked; the hit point
 // and attributes are recomputed for the winner, which is bit-identical to
 // the reference's eager copies (same t, same expressions).
-__device__ __forceinline__ bool polygon_edges(const float* __restrict__ q, int nv, f3 P) {
+__device__ __forceinline__ bool polygon_edges(const __attribute__((address_space(4))) float* q, int nv, f3 P) {
     // q points at {v0[3], in0[3], v1[3], in1[3], ...}; reject if any
     // dot(inner_k, P - v_k) < 0 (Intersection.cuh:130-134 / :165-170)
     bool inside = true;
@@ -245,7 +245,7 @@ __device__ __forceinline__ bool polygon_edges(const float* __restrict__ q, int n
     return inside;
 }
 
-__device__ __forceinline__ void polygon_test(const float* __restrict__ q, int nv, f3 o, f3 d, int id,
+__device__ __forceinline__ void polygon_test(const __attribute__((address_space(4))) float* q, int nv, f3 o, f3 d, int id,
                                              float& best_t, int& best_id) {
     float nx = q[0], ny = q[1], nz = q[2], dd = q[3];
     float nd = nx * d.x + ny * d.y + nz * d.z;
@@ -264,6 +264,14 @@ __device__ __forceinline__ void polygon_test(const float* __restrict__ q, int nv
     }
 }
 
+// Scene records are read-only for the whole launch and indexed wave-
+// uniformly: read them through the constant address space so they come in
+// through scalar loads (s_load_dword*) into SGPRs even though the kernel
+// stores to global memory inside the loop (which would otherwise make the
+// compiler fall back to per-lane vector loads with a full vmcnt wait).
+typedef const __attribute__((address_space(4))) float* cfloat_ptr;
+__device__ __forceinline__ cfloat_ptr as_const(const float* p) { return (cfloat_ptr)p; }
+
 __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
     const float a = dot(d, d);
     const float a4 = 4.0f * a;
@@ -273,9 +281,15 @@ __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, flo
     const int pln_base = K.n_sph;
     const int tri_base = K.n_sph + K.n_pln;
     const int quad_base = tri_base + K.n_tri;
+#ifdef RT_UNROLL_MAXN
+#pragma unroll
+    for (int i = 0; i < RT_UNROLL_MAXN; i++) {
+        if (i >= K.n_max) break;
+#else
     for (int i = 0; i < K.n_max; i++) {
+#endif
         if (i < K.n_sph) {  // Intersection.cuh:15-62
-            const float* s = K.sph + RT_SPH_FLOATS * i;
+            const cfloat_ptr s = as_const(K.sph) + RT_SPH_FLOATS * i;
             f3 xp = mk(o.x - s[0], o.y - s[1], o.z - s[2]);
             float b = 2.0f * dot(xp, d);
             float c = dot(xp, xp) - s[3];
@@ -291,7 +305,7 @@ __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, flo
             }
         }
         if (i < K.n_pln) {  // Intersection.cuh:64-106
-            const float* q = K.pln + RT_PLN_FLOATS * i;
+            const cfloat_ptr q = as_const(K.pln) + RT_PLN_FLOATS * i;
             float nx = q[0], ny = q[1], nz = q[2], dd = q[3];
             float nd = nx * d.x + ny * d.y + nz * d.z;
             if (!(fabsf(nd) < RT_NEAR_ZERO)) {
@@ -302,8 +316,8 @@ __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, flo
                 }
             }
         }
-        if (i < K.n_tri) polygon_test(K.tri + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, best_t, best_id);
-        if (i < K.n_quad) polygon_test(K.quad + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, best_t, best_id);
+        if (i < K.n_tri) polygon_test(as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, best_t, best_id);
+        if (i < K.n_quad) polygon_test(as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, best_t, best_id);
     }
 }
 
@@ -388,6 +402,65 @@ __device__ __forceinline__ void store_pixel(const rt_kparams& K, long npix, cons
     if (K.rgba) K.rgba[p] = tone_map(s.ax, s.ay, s.az, s.frame - 1u);
 }
 
+// Specular branch of tracePath after the brdfChoice draw (Main.cu:245-255):
+// microfacet normal (genMicrofacetNormal :170-185) in the tangent frame
+// (baseAroundNormalToRegular :149-168), mirror reflection (:187-191),
+// Fresnel (:122-133) and the G-term weight (:112-147).  Returns the scatter
+// direction; kspec = specularTerm * fresnelTerm / specularChance.
+__device__ __forceinline__ f3 specular_scatter(Xorwow& rs, f3 d, f3 n, float rough, float rough2,
+                                               float ior2m1, float& kspec) {
+    const float e1 = rand_range(rs, 1.0f);
+    const float e2 = rand_range(rs, 1.0f);
+    const float theta = atan_nn(rough * sqrtf(e1) / sqrtf(1.0f - e1));
+    const float phi = 2.0f * RT_PI * e2;
+    float st, ct, sp, cp;
+    sincos_nn(theta, st, ct);
+    sincos_nn(phi, sp, cp);
+    const f3 mloc = mk(st * cp, st * sp, ct);
+    f3 some = mk(1.0f, 0.0f, 0.0f);
+    if (fabsf(dot(n, some)) < 1.0f - RT_NEAR_ZERO) some = mk(0.0f, 1.0f, 0.0f);
+    const f3 t1 = cross(n, some);
+    const f3 t2 = cross(n, t1);
+    const f3 m = mk(dot(mk(t1.x, t2.x, n.x), mloc), dot(mk(t1.y, t2.y, n.y), mloc),
+                    dot(mk(t1.z, t2.z, n.z), mloc));
+    const f3 scatter = sub(d, scale(2.0f * dot(d, m), m));
+    const f3 inc = scale(-1.0f, d);
+    const float fr = fresnel(inc, m, ior2m1);
+    const float sw = specular_weight(inc, scatter, n, m, rough2);
+    kspec = sw * fr / RT_SPECULAR_CHANCE;
+    return scatter;
+}
+
+// Fold of the recursion innermost-first (Main.cu:262-268):
+//   L = emitted + (brdf * L) * cosAngle,  emitted = emittance * albedo,
+//   brdf = kspec * {1,1,1} (specular) or 4 * albedo (diffuse, :259).
+template <int BLOCK>
+__device__ __forceinline__ void fold_records(const int* rec_code, const float* rec_k, const float* rec_c,
+                                             int depth, const float* hit_tab, float& lx, float& ly,
+                                             float& lz) {
+    lx = 0.0f;
+    ly = 0.0f;
+    lz = 0.0f;  // backgroundColor
+    for (int l = depth - 1; l >= 0; --l) {
+        const int c0 = rec_code[l * BLOCK];
+        const float k = rec_k[l * BLOCK];
+        const float c = rec_c[l * BLOCK];
+        const bool spec = c0 < 0;
+        const float4 mat = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * (spec ? ~c0 : c0) + 4);
+        const float ex = mat.w * mat.x, ey = mat.w * mat.y, ez = mat.w * mat.z;
+        const float dk = (float)(2.0 / (1 - RT_SPECULAR_CHANCE));  // 4.0f
+        const float bx = spec ? k : dk * mat.x, by = spec ? k : dk * mat.y, bz = spec ? k : dk * mat.z;
+        lx = ex + (bx * lx) * c;
+        ly = ey + (by * ly) * c;
+        lz = ez + (bz * lz) * c;
+    }
+}
+
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
 }  // namespace
 
 // LDS layout: [hit table, n_prim*12 floats, if HIT_LDS] then the record stack
@@ -431,14 +504,34 @@ rt_render_kernel(rt_kparams K) {
     int depth = -1;  // -1: needs a camera ray for its next frame
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
 
+#ifdef RT_STAMPS
+    unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
+#define STAMP(k)                                              \
+    do {                                                      \
+        unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+        st_acc[k] += _t - st_prev;                            \
+        st_prev = _t;                                         \
+    } while (0)
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
     while (true) {
+        STAMP(4);
         // (1) regenerate: jittered camera ray (Main.cu:290-292)
         if (depth < 0 && px.passes_left > 0) {
+#ifdef RT_ABL_NOJITTER
+            f3 jit = px.d0;
+#else
             f3 jit = random_direction(px.rs, px.d0);
+#endif
             d = normalize3(add(px.d0, scale(K.jitter, jit)));
             o = cam;
             depth = 0;
         }
+        STAMP(0);
         const bool active = depth >= 0;
         if (__ballot(active) == 0ull) break;
         if (active) {
@@ -446,6 +539,7 @@ rt_render_kernel(rt_kparams K) {
             float t;
             int id;
             closest_hit(K, o, d, t, id);
+            STAMP(1);
 
             bool finished = true;
             if (id >= 0) {
@@ -464,7 +558,15 @@ rt_render_kernel(rt_kparams K) {
                 int code = id;
                 float kspec = 0.0f;
                 const float choice = rand_range(px.rs, 1.0f);
+#if defined(RT_ABL_NOSHADE)
+                if (false) {
+#elif defined(RT_ABL_ALLSPEC)
+                if (true) {
+#elif defined(RT_ABL_ALLDIFF)
+                if (false) {
+#else
                 if (choice < RT_SPECULAR_CHANCE) {
+#endif
                     // genMicrofacetNormal (Main.cu:170-185)
                     const float e1 = rand_range(px.rs, 1.0f);
                     const float e2 = rand_range(px.rs, 1.0f);
@@ -488,7 +590,11 @@ rt_render_kernel(rt_kparams K) {
                     kspec = sw * fr / RT_SPECULAR_CHANCE;  // brdf = (s*F/0.5) * {1,1,1}
                     code = ~id;
                 } else {
+#if defined(RT_ABL_NOSHADE)
+                    scatter = sub(d, scale(2.0f * dot(d, n), n));
+#else
                     scatter = random_direction(px.rs, n);  // brdf = 4 * albedo
+#endif
                 }
                 (void)albedo;
                 rec_code[depth * BLOCK] = code;
@@ -499,6 +605,7 @@ rt_render_kernel(rt_kparams K) {
                 d = scatter;
                 finished = depth > K.max_bounces;  // Main.cu:210
             }
+            STAMP(2);
             if (finished) {
                 // (4) fold the recursion innermost-first (Main.cu:262-268):
                 //     L = emitted + (brdf * L) * cosAngle
@@ -533,8 +640,14 @@ rt_render_kernel(rt_kparams K) {
                     load_pixel(K, npix, px.p + T, px);
                 }
             }
+            STAMP(3);
         }
     }
+#ifdef RT_STAMPS
+    if ((threadIdx.x & 63) == 0 && K.stamps)
+        for (int k = 0; k < 5; k++) atomicAdd(&K.stamps[k], st_acc[k]);
+#endif
+#undef STAMP
 }
 
 // initializeRand (Main.cu:369-380): curand_init(y*W + x, 0, 0)
@@ -573,55 +686,314 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
     image[q] = gathered[((long)r * rows_per_shard + j) * width + x];
 }
 
+
+// ===========================================================================
+// Sorted task-queue megakernel (the product path).
+//
+// Divergence, not memory, bounds the simple one-path-per-lane kernel: in a
+// wave, lanes that need a camera ray, a specular bounce or a diffuse bounce
+// execute all three code paths one after the other (rocprof: 20 of 64 lanes
+// active per VALU instruction).  Here each workgroup iterates in lock-step:
+//
+//   T-phase: every lane with pending work posts ONE task into an LDS queue:
+//            RANDDIR tasks (camera-jitter direction for a new frame, or a
+//            diffuse bounce: both are genRandomDirection, Main.cu:193-206)
+//            fill slots from the front, SPEC tasks (Main.cu:245-255) from
+//            the back; wave w then executes slots 64w..64w+63, so each wave
+//            runs one task kind (at most one wave holds both).  The task
+//            carries the lane's RNG state (6 x u32) and returns it updated,
+//            so every pixel still consumes its own stream in reference order.
+//   I-phase: every lane with a ray runs closest_hit (uniform code), draws its
+//            brdfChoice, and posts the shading task for the next T-phase; a
+//            miss (or the depth limit) folds the path's records, accumulates
+//            the frame and schedules the pixel's next camera ray.
+//
+// LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
+//      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
+template <int BLOCK, bool HIT_LDS>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
+rt_render_sorted_kernel(rt_kparams K) {
+    enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
+    enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };
+    extern __shared__ float smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    const float* hit_tab = K.hit;
+    float* rec_base = smem;
+    if (HIT_LDS) {
+        for (int i = tid; i < n_prim * RT_HIT_FLOATS; i += BLOCK) smem[i] = K.hit[i];
+        hit_tab = smem;
+        rec_base = smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3);
+    }
+    const int levels = K.max_bounces + 1;
+    int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
+    float* rec_k = rec_base + levels * BLOCK + tid;
+    float* rec_c = rec_base + 2 * levels * BLOCK + tid;
+    float* slots = rec_base + 3 * levels * BLOCK;
+    int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
+    if (tid < 4) counters[tid] = 0;
+    __syncthreads();
+#define SLOT(f, i) slots[(f) * BLOCK + (i)]
+
+    const long npix = (long)K.rows * K.width;
+    const long T = (long)gridDim.x * BLOCK;
+    PixelState px;
+    load_pixel(K, npix, (long)blockIdx.x * BLOCK + tid, px);
+    int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
+
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+    f3 hP = o, hn = o;  // pending hit: point, normal
+    int hid = 0, depth = 0;
+    bool hspec = false, has_ray = false;
+    int parity = 0;
+    const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
+
+    // path end: fold, accumulate (Main.cu:299-304), next frame / next pixel
+    auto finish_path = [&]() {
+        float lx, ly, lz;
+        fold_records<BLOCK>(rec_code, rec_k, rec_c, depth, hit_tab, lx, ly, lz);
+        if (px.frame == 1u) {
+            px.ax = 0.0f;
+            px.ay = 0.0f;
+            px.az = 0.0f;
+        }
+        px.ax = px.ax + lx;
+        px.ay = px.ay + ly;
+        px.az = px.az + lz;
+        px.frame++;
+        px.passes_left--;
+        if (px.passes_left == 0) {
+            store_pixel(K, npix, px);
+            load_pixel(K, npix, px.p + T, px);
+        }
+        mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
+    };
+
+#ifdef RT_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(k)                                              \
+    do {                                                      \
+        unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+        st_acc[k] += _t - st_prev;                            \
+        st_prev = _t;                                         \
+    } while (0)
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+    while (true) {
+        const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
+        STAMP(7);
+        if (!__syncthreads_or(task != T_NONE)) break;
+        STAMP(0);
+
+        // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
+        int* cnt = counters + 2 * parity;
+        const bool front = task == T_REGEN || task == T_DIFF;
+        const unsigned long long mf = __ballot(front);
+        const unsigned long long mbk = __ballot(task == T_SPEC);
+        int base_f = 0, base_b = 0;
+        if (lane == 0) {
+            if (mf) base_f = atomicAdd(&cnt[0], __popcll(mf));
+            if (mbk) base_b = atomicAdd(&cnt[1], __popcll(mbk));
+        }
+        base_f = __builtin_amdgcn_readfirstlane(base_f);
+        base_b = __builtin_amdgcn_readfirstlane(base_b);
+        int slot = -1;
+        if (front) slot = base_f + lanes_below(mf);
+        if (task == T_SPEC) slot = BLOCK - 1 - (base_b + lanes_below(mbk));
+        if (slot >= 0) {
+            const f3 nrm = task == T_REGEN ? px.d0 : hn;
+            SLOT(0, slot) = nrm.x;
+            SLOT(1, slot) = nrm.y;
+            SLOT(2, slot) = nrm.z;
+            SLOT(3, slot) = d.x;
+            SLOT(4, slot) = d.y;
+            SLOT(5, slot) = d.z;
+            SLOT(6, slot) = __int_as_float(task == T_REGEN ? -1 : hid);
+            SLOT(7, slot) = __uint_as_float(px.rs.d);
+            SLOT(8, slot) = __uint_as_float(px.rs.v0);
+            SLOT(9, slot) = __uint_as_float(px.rs.v1);
+            SLOT(10, slot) = __uint_as_float(px.rs.v2);
+            SLOT(11, slot) = __uint_as_float(px.rs.v3);
+            SLOT(12, slot) = __uint_as_float(px.rs.v4);
+        }
+        STAMP(1);
+        __syncthreads();
+        STAMP(2);
+
+        // ---- T-phase: execute slot `tid`
+        {
+            const int nf = cnt[0], nb = cnt[1];
+            const bool do_front = tid < nf;
+            const bool do_spec = tid >= BLOCK - nb;
+            if (do_front || do_spec) {
+                Xorwow rs;
+                rs.d = __float_as_uint(SLOT(7, tid));
+                rs.v0 = __float_as_uint(SLOT(8, tid));
+                rs.v1 = __float_as_uint(SLOT(9, tid));
+                rs.v2 = __float_as_uint(SLOT(10, tid));
+                rs.v3 = __float_as_uint(SLOT(11, tid));
+                rs.v4 = __float_as_uint(SLOT(12, tid));
+                const f3 nrm = mk(SLOT(0, tid), SLOT(1, tid), SLOT(2, tid));
+                const int code = __float_as_int(SLOT(6, tid));
+                f3 r;
+                if (do_front) {
+                    r = random_direction(rs, nrm);
+                    if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
+                } else {
+                    const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
+                    const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
+                    float kspec;
+                    r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
+                    SLOT(3, tid) = kspec;
+                }
+                SLOT(0, tid) = r.x;
+                SLOT(1, tid) = r.y;
+                SLOT(2, tid) = r.z;
+                SLOT(7, tid) = __uint_as_float(rs.d);
+                SLOT(8, tid) = __uint_as_float(rs.v0);
+                SLOT(9, tid) = __uint_as_float(rs.v1);
+                SLOT(10, tid) = __uint_as_float(rs.v2);
+                SLOT(11, tid) = __uint_as_float(rs.v3);
+                SLOT(12, tid) = __uint_as_float(rs.v4);
+            }
+        }
+        STAMP(3);
+        __syncthreads();
+        STAMP(4);
+        if (tid == 0) {
+            counters[2 * (parity ^ 1)] = 0;
+            counters[2 * (parity ^ 1) + 1] = 0;
+        }
+        parity ^= 1;
+
+        // ---- owner: take the task result back
+        if (slot >= 0) {
+            const f3 r = mk(SLOT(0, slot), SLOT(1, slot), SLOT(2, slot));
+            px.rs.d = __float_as_uint(SLOT(7, slot));
+            px.rs.v0 = __float_as_uint(SLOT(8, slot));
+            px.rs.v1 = __float_as_uint(SLOT(9, slot));
+            px.rs.v2 = __float_as_uint(SLOT(10, slot));
+            px.rs.v3 = __float_as_uint(SLOT(11, slot));
+            px.rs.v4 = __float_as_uint(SLOT(12, slot));
+            mode = M_IDLE;
+            if (task == T_REGEN) {
+                o = cam;
+                d = r;
+                depth = 0;
+                has_ray = true;
+            } else {
+                rec_code[depth * BLOCK] = task == T_SPEC ? ~hid : hid;
+                rec_k[depth * BLOCK] = task == T_SPEC ? SLOT(3, slot) : 0.0f;
+                rec_c[depth * BLOCK] = dot(r, hn);  // cosAngle, Main.cu:264
+                depth++;
+                o = hP;
+                d = r;
+                if (depth > K.max_bounces)  // Main.cu:210
+                    finish_path();
+                else
+                    has_ray = true;
+            }
+        }
+
+        STAMP(5);
+        // ---- I-phase: closest hit + brdfChoice (Main.cu:214-245)
+        if (has_ray) {
+            has_ray = false;
+            float t;
+            int id;
+            closest_hit(K, o, d, t, id);
+            if (id >= 0) {
+                const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
+                hP = add(o, scale(t, d));
+                hn = mk(h0.x, h0.y, h0.z);
+                if (h0.w != 0.0f) hn = normalize3(sub(hP, hn));  // sphere normal
+                hid = id;
+                hspec = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE;
+                mode = M_SHADE;
+            } else {
+                finish_path();
+            }
+        }
+        STAMP(6);
+    }
+#ifdef RT_STAMPS
+    if ((threadIdx.x & 63) == 0 && K.stamps)
+        for (int k = 0; k < 8; k++) atomicAdd(&K.stamps[k], st_acc[k]);
+#endif
+#undef STAMP
+#undef SLOT
+}
+
 // ---- launchers (host side) ------------------------------------------------
 namespace {
-template <int BLOCK, bool HIT_LDS>
-hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_cap, hipStream_t stream) {
+template <int BLOCK, bool HIT_LDS, bool SORTED>
+void* kernel_ptr() {
+    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS>)
+                  : reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS>);
+}
+
+template <int BLOCK, bool HIT_LDS, bool SORTED>
+hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
     const long npix = (long)K.rows * K.width;
     long grid = (npix + BLOCK - 1) / BLOCK;
-    if (grid_cap > 0 && grid > grid_cap) grid = grid_cap;
+    if (grid_mult > 0) {  // persistent: grid_mult x resident workgroups per CU x CUs
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED>(), BLOCK, lds) ==
+                hipSuccess &&
+            per_cu > 0) {
+            const long cap = (long)per_cu * num_cus * grid_mult;
+            if (grid > cap) grid = cap;
+        }
+    }
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+    if (SORTED)
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+    else
+        hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
     return hipGetLastError();
 }
 
-template <int BLOCK, bool HIT_LDS>
-int resident_blocks_per_cu(size_t lds) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rt_render_kernel<BLOCK, HIT_LDS>, BLOCK, lds) != hipSuccess)
-        return 0;
-    return n;
+template <int BLOCK, bool SORTED>
+hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s) {
+    return hit_lds ? launch_render<BLOCK, true, SORTED>(K, lds, grid_mult, num_cus, s)
+                   : launch_render<BLOCK, false, SORTED>(K, lds, grid_mult, num_cus, s);
 }
 }  // namespace
 
 // LDS bytes of one workgroup: hit table (if staged) + 3 record dwords per
-// level per lane.
-size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds) {
+// level per lane (+ 13 task-slot dwords per lane and 4 counters, sorted).
+size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
-    return hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
+    size_t b = hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
+    if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
+    return b;
 }
 
-// Host-side launch policy: 256-lane workgroups (64 for very deep paths),
-// hit table in LDS when it fits in 16 KB, persistent grid of
-// waves_per_cu-many resident workgroups per CU (0 = one per 256 pixels).
-hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, hipStream_t stream) {
+// Host-side launch policy: 256-lane workgroups (64 when the record stack of
+// very deep paths would not fit), hit table in LDS when it fits in 16 KB,
+// sorted task-queue kernel unless `simple`; grid_mult > 0 caps the grid at
+// grid_mult x resident workgroups per CU (persistent lanes).
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, hipStream_t stream) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
-    const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 32768;
+    const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 49152;
     const int block = small_block ? 64 : 256;
-    const size_t lds = rt_render_lds_bytes(K, block, hit_lds);
-    int per_cu = 0;
-    if (grid_mult > 0) {
-        if (small_block)
-            per_cu = hit_lds ? resident_blocks_per_cu<64, true>(lds) : resident_blocks_per_cu<64, false>(lds);
-        else
-            per_cu = hit_lds ? resident_blocks_per_cu<256, true>(lds) : resident_blocks_per_cu<256, false>(lds);
-    }
-    const int cap = (grid_mult > 0 && per_cu > 0) ? per_cu * num_cus * grid_mult : 0;
-    if (small_block)
-        return hit_lds ? launch_render<64, true>(K, lds, cap, stream) : launch_render<64, false>(K, lds, cap, stream);
-    return hit_lds ? launch_render<256, true>(K, lds, cap, stream) : launch_render<256, false>(K, lds, cap, stream);
+    const size_t lds = rt_render_lds_bytes(K, block, hit_lds, !simple);
+    if (simple)
+        return small_block ? launch_block<64, false>(K, hit_lds, lds, grid_mult, num_cus, stream)
+                           : launch_block<256, false>(K, hit_lds, lds, grid_mult, num_cus, stream);
+#ifndef RT_SORTED_BLOCK
+#define RT_SORTED_BLOCK 256
+#endif
+    if (small_block) return launch_block<64, true>(K, hit_lds, lds, grid_mult, num_cus, stream);
+    const size_t lds_s = rt_render_lds_bytes(K, RT_SORTED_BLOCK, hit_lds, true);
+    return launch_block<RT_SORTED_BLOCK, true>(K, hit_lds, lds_s, grid_mult, num_cus, stream);
 }
 
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,

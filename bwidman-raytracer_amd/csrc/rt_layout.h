@@ -57,4 +57,5 @@ struct rt_kparams {
     unsigned* rng;              // 6 planes of rows*width
     float* accum;               // 3 planes of rows*width
     unsigned* rgba;             // rows*width (may be null)
+    unsigned long long* stamps; // diagnostic builds (-DRT_STAMPS) only: per-phase cycle sums
 };
