@@ -182,7 +182,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (round(traffic["hbm_bytes_per_launch"]) if traffic else None),
-                         "kernel": "rt_render_kernel",
+                         "kernel": "rt_render_sorted_kernel",
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "bytes_per_unit": BYTES_PER_PIXEL_PASS, "units_per_launch": units},
         }
