@@ -11,7 +11,6 @@
 // the reference's order, so the kernel sees bit-identical inputs.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -80,11 +79,6 @@ struct rt_context {
     rt_camera camera{};
     int n_sph = 0, n_pln = 0, n_tri = 0, n_quad = 0;
     DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table
-    std::vector<double> bounds;  // per primitive {cx, cy, cz, R} (R < 0: unbounded, e.g. planes)
-    DevBuf cull_buf;             // per primitive {u.xyz, cos threshold} for the current camera
-    bool cull_valid = false;
-    rt_camera cull_cam{};
-    float cull_jitter = -1.0f;
     size_t off_pln = 0, off_tri = 0, off_quad = 0, off_hit = 0;  // in floats
 
     // shard state
@@ -229,7 +223,6 @@ void rt_destroy(rt_context* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->last_stream && c->last_stream != c->stream) (void)hipStreamSynchronize(c->last_stream);
     free_buf(c->scene_buf);
-    free_buf(c->cull_buf);
     free_buf(c->rng);
     free_buf(c->accum);
     free_buf(c->rgba);
@@ -307,34 +300,6 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     c->off_hit = off_hit;
     c->camera = s->camera;
     c->has_scene = true;
-    c->cull_valid = false;
-    // bounding spheres for the primary-ray candidate masks (rt_kernels.hip)
-    c->bounds.assign((size_t)(ns + np + nt + nq) * 4, 0.0);
-    {
-        size_t k = 0;
-        auto put = [&](double x, double y, double z, double r) {
-            c->bounds[4 * k] = x;
-            c->bounds[4 * k + 1] = y;
-            c->bounds[4 * k + 2] = z;
-            c->bounds[4 * k + 3] = r;
-            k++;
-        };
-        auto poly = [&](const rt_vec3* v, int nv) {
-            double cx = 0, cy = 0, cz = 0, r = 0;
-            for (int i = 0; i < nv; i++) cx += v[i].x, cy += v[i].y, cz += v[i].z;
-            cx /= nv, cy /= nv, cz /= nv;
-            for (int i = 0; i < nv; i++)
-                r = std::max(r, std::sqrt((v[i].x - cx) * (v[i].x - cx) + (v[i].y - cy) * (v[i].y - cy) +
-                                          (v[i].z - cz) * (v[i].z - cz)));
-            put(cx, cy, cz, r);
-        };
-        for (int i = 0; i < ns; i++)
-            put(s->spheres[i].position.x, s->spheres[i].position.y, s->spheres[i].position.z,
-                std::fabs((double)s->spheres[i].radius));
-        for (int i = 0; i < np; i++) put(0, 0, 0, -1.0);
-        for (int i = 0; i < nt; i++) poly(s->triangles[i].vertices, 3);
-        for (int i = 0; i < nq; i++) poly(s->quads[i].vertices, 4);
-    }
     c->frame = 1;
     return RT_OK;
 }
@@ -342,7 +307,6 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
 int rt_set_camera(rt_context* c, const rt_camera* cam) {
     if (!c || !cam) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
     c->camera = *cam;
-    c->cull_valid = false;
     c->frame = 1;  // Controls.cuh: any movement sets accumulatedFrames = 1
     return RT_OK;
 }
@@ -456,45 +420,6 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.hit = base + c->off_hit;
     K.rng = (unsigned*)c->rng.p;
     K.accum = (float*)c->accum.p;
-    K.cull = nullptr;
-    const int n_prim = c->n_sph + c->n_pln + c->n_tri + c->n_quad;
-    if (n_prim > 0 && n_prim <= 32 && !std::getenv("BWRT_NO_CULL")) {
-        if (!c->cull_valid || c->cull_jitter != K.jitter ||
-            std::memcmp(&c->cull_cam, &c->camera, sizeof c->camera) != 0) {
-            // Primary-ray candidate table.  Every jittered camera ray of a
-            // pixel is within theta of d0 (|jitter * r| <= jitter, r unit);
-            // a primitive can only be hit through its bounding sphere,
-            // inflated far beyond float rounding; seen from the camera it
-            // spans beta = asin(R/L).  Candidate iff dot(d0, u) >= cos(beta +
-            // theta + margin) (minus slack for the float dot product).
-            const double theta = std::asin(std::min(1.0, 1.02 * (double)K.jitter)) + 1e-5;
-            std::vector<float> tab((size_t)n_prim * 4);
-            for (int k = 0; k < n_prim; k++) {
-                const double* b = &c->bounds[4 * (size_t)k];
-                float* t = &tab[4 * (size_t)k];
-                const double vx = b[0] - cam.position.x, vy = b[1] - cam.position.y, vz = b[2] - cam.position.z;
-                const double L = std::sqrt(vx * vx + vy * vy + vz * vz);
-                const double R = b[3] * (1.0 + 1e-3) + 1e-3 + 1e-4 * L;
-                if (b[3] < 0.0 || L <= R) {  // unbounded, or the camera inside: always a candidate
-                    t[0] = t[1] = t[2] = 0.0f;
-                    t[3] = -2.0f;
-                    continue;
-                }
-                const double ang = std::asin(R / L) + theta + 1e-5;
-                t[0] = (float)(vx / L);
-                t[1] = (float)(vy / L);
-                t[2] = (float)(vz / L);
-                t[3] = ang >= 3.141592653589793 ? -2.0f : (float)(std::cos(ang) - 1e-6);
-            }
-            int rc = ensure_buf(c, c->cull_buf, tab.size() * sizeof(float));
-            if (rc) return rc;
-            HIP_TRY(c, hipMemcpy(c->cull_buf.p, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
-            c->cull_valid = true;
-            c->cull_cam = c->camera;
-            c->cull_jitter = K.jitter;
-        }
-        K.cull = (const float*)c->cull_buf.p;
-    }
     return RT_OK;
 }
 

@@ -690,99 +690,30 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 // ===========================================================================
 // Sorted task-queue megakernel (the product path).
 //
-// Divergence, not memory, bounds a one-path-per-lane kernel: in a wave, lanes
-// that need a camera ray, a specular bounce or a diffuse bounce execute all
-// three code paths one after the other.  Here each workgroup iterates in
-// lock-step:
+// Divergence, not memory, bounds the simple one-path-per-lane kernel: in a
+// wave, lanes that need a camera ray, a specular bounce or a diffuse bounce
+// execute all three code paths one after the other (rocprof: 20 of 64 lanes
+// active per VALU instruction).  Here each workgroup iterates in lock-step:
 //
-//   T-phase: every lane with pending work posts ONE task into an LDS queue,
-//            grouped by kind (REGEN | DIFF | SPEC, counted before the
-//            loop-top barrier, one LDS atomic per wave and kind); wave w then
-//            executes slots 64w..64w+63, so waves run one task kind.  The
-//            task carries the lane's RNG state (6 x u32) and returns it, so
-//            every pixel consumes its own stream in reference order.
-//              REGEN: camera jitter (Main.cu:290-292) + the PRIMARY closest
-//                     hit, tested only against the pixel's candidate
-//                     primitives (below);
-//              DIFF : genRandomDirection about the normal (Main.cu:258);
-//              SPEC : microfacet specular bounce (Main.cu:245-255).
-//   I-phase: every lane with a secondary ray runs closest_hit; hits draw
-//            brdfChoice and post their shading task; a miss (or the depth
-//            limit) folds the path's records, accumulates the frame and
-//            posts the pixel's next REGEN.
-//
-// Primary-ray candidates: all jittered camera rays of a pixel lie in a cone
-// of half-angle ~asin(jitter) around d0 = normalize(rot * pixelPosition).
-// The host builds, per primitive, a bounding sphere inflated well beyond
-// float rounding and the cosine threshold of (its angular radius + the cone
-// angle + margin) seen from the camera; a pixel's candidate mask is
-// {k : dot(d0, u_k) >= thr_k}.  A primitive outside the mask cannot pass the
-// reference's hit test for any of the pixel's primary rays, so testing only
-// candidates (in the reference's interleaved order) yields the identical
-// winner and t.  Scenes with > 32 primitives use the full test.
+//   T-phase: every lane with pending work posts ONE task into an LDS queue:
+//            RANDDIR tasks (camera-jitter direction for a new frame, or a
+//            diffuse bounce: both are genRandomDirection, Main.cu:193-206)
+//            fill slots from the front, SPEC tasks (Main.cu:245-255) from
+//            the back; wave w then executes slots 64w..64w+63, so each wave
+//            runs one task kind (at most one wave holds both).  The task
+//            carries the lane's RNG state (6 x u32) and returns it updated,
+//            so every pixel still consumes its own stream in reference order.
+//   I-phase: every lane with a ray runs closest_hit (uniform code), draws its
+//            brdfChoice, and posts the shading task for the next T-phase; a
+//            miss (or the depth limit) folds the path's records, accumulates
+//            the frame and schedules the pixel's next camera ray.
 //
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
-//      [task slots 16 x BLOCK, field-major][2 x 3 queue counters]
-#define RT_SLOT_FIELDS 16
-__device__ __forceinline__ void closest_hit_masked(const rt_kparams& K, f3 o, f3 d, unsigned mask,
-                                                   float& best_t, int& best_id) {
-    const float a = dot(d, d);
-    const float a4 = 4.0f * a;
-    const float a2 = 2.0f * a;
-    best_t = INFINITY;
-    best_id = -1;
-    const int pln_base = K.n_sph;
-    const int tri_base = K.n_sph + K.n_pln;
-    const int quad_base = tri_base + K.n_tri;
-    for (int i = 0; i < K.n_max; i++) {
-        if (i < K.n_sph && ((mask >> i) & 1u)) {
-            const cfloat_ptr s = as_const(K.sph) + RT_SPH_FLOATS * i;
-            f3 xp = mk(o.x - s[0], o.y - s[1], o.z - s[2]);
-            float b = 2.0f * dot(xp, d);
-            float c = dot(xp, xp) - s[3];
-            float disc = b * b - a4 * c;
-            if (!(disc < 0.0f) && !(b >= 0.0f && disc == disc && a2 > 0.0f)) {
-                float t = (-b - sqrtf(disc)) / a2;
-                if (!(t <= RT_NEAR_ZERO || t > best_t)) {
-                    best_t = t;
-                    best_id = i;
-                }
-            }
-        }
-        if (i < K.n_pln && ((mask >> (pln_base + i)) & 1u)) {
-            const cfloat_ptr q = as_const(K.pln) + RT_PLN_FLOATS * i;
-            float nx = q[0], ny = q[1], nz = q[2], dd = q[3];
-            float nd = nx * d.x + ny * d.y + nz * d.z;
-            if (!(fabsf(nd) < RT_NEAR_ZERO)) {
-                float t = -((nx * o.x + ny * o.y + nz * o.z) + dd) / nd;
-                if (!(t <= RT_NEAR_ZERO || t > best_t)) {
-                    best_t = t;
-                    best_id = pln_base + i;
-                }
-            }
-        }
-        if (i < K.n_tri && ((mask >> (tri_base + i)) & 1u))
-            polygon_test(as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, best_t, best_id);
-        if (i < K.n_quad && ((mask >> (quad_base + i)) & 1u))
-            polygon_test(as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, best_t, best_id);
-    }
-}
-
-__device__ __forceinline__ unsigned primary_candidates(const rt_kparams& K, f3 d0) {
-    // NaN rays are accepted by every hit test (t compares false): no culling
-    if (!K.cull || !(d0.x == d0.x && d0.y == d0.y && d0.z == d0.z)) return 0xffffffffu;
-    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
-    unsigned m = 0u;
-    for (int k = 0; k < n_prim; k++) {
-        const cfloat_ptr c = as_const(K.cull) + 4 * k;
-        if (d0.x * c[0] + d0.y * c[1] + d0.z * c[2] >= c[3]) m |= 1u << k;
-    }
-    return m;
-}
-
+//      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
 template <int BLOCK, bool HIT_LDS>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
+    enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
     enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
@@ -800,8 +731,8 @@ rt_render_sorted_kernel(rt_kparams K) {
     float* rec_k = rec_base + levels * BLOCK + tid;
     float* rec_c = rec_base + 2 * levels * BLOCK + tid;
     float* slots = rec_base + 3 * levels * BLOCK;
-    int* counters = reinterpret_cast<int*>(slots + RT_SLOT_FIELDS * BLOCK);  // [parity][kind-1]
-    if (tid < 6) counters[tid] = 0;
+    int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
+    if (tid < 4) counters[tid] = 0;
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
 
@@ -809,29 +740,14 @@ rt_render_sorted_kernel(rt_kparams K) {
     const long T = (long)gridDim.x * BLOCK;
     PixelState px;
     load_pixel(K, npix, (long)blockIdx.x * BLOCK + tid, px);
-    unsigned cand = px.valid ? primary_candidates(K, px.d0) : 0u;
+    int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     f3 hP = o, hn = o;  // pending hit: point, normal
     int hid = 0, depth = 0;
-    int task = px.passes_left > 0 ? T_REGEN : T_NONE;
+    bool hspec = false, has_ray = false;
     int parity = 0;
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
-
-    // count this lane's next task into the queue counters of `par`: one LDS
-    // atomic per wave and kind; returns this lane's offset within its kind
-    auto count_task = [&](int par) -> int {
-        int off = 0;
-#pragma unroll
-        for (int k = 1; k <= 3; k++) {
-            const unsigned long long m = __ballot(task == k);
-            int base = 0;
-            if (lane == 0 && m) base = atomicAdd(&counters[3 * par + k - 1], __popcll(m));
-            base = __builtin_amdgcn_readfirstlane(base);
-            if (task == k) off = base + lanes_below(m);
-        }
-        return off;
-    };
 
     // path end: fold, accumulate (Main.cu:299-304), next frame / next pixel
     auto finish_path = [&]() {
@@ -850,36 +766,45 @@ rt_render_sorted_kernel(rt_kparams K) {
         if (px.passes_left == 0) {
             store_pixel(K, npix, px);
             load_pixel(K, npix, px.p + T, px);
-            if (px.valid) cand = primary_candidates(K, px.d0);
         }
-        task = px.passes_left > 0 ? T_REGEN : T_NONE;
+        mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
     };
 
-    // closest-hit result of a ray from o along d at bounce `depth`
-    auto take_hit = [&](float t, int id) {
-        if (id >= 0) {
-            const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
-            hP = add(o, scale(t, d));
-            hn = mk(h0.x, h0.y, h0.z);
-            if (h0.w != 0.0f) hn = normalize3(sub(hP, hn));  // sphere normal
-            hid = id;
-            task = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE ? T_SPEC : T_DIFF;  // brdfChoice
-        } else {
-            finish_path();
-        }
-    };
-
-    int my_off = count_task(parity);
+#ifdef RT_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(k)                                              \
+    do {                                                      \
+        unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+        st_acc[k] += _t - st_prev;                            \
+        st_prev = _t;                                         \
+    } while (0)
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
     while (true) {
+        const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
+        STAMP(7);
         if (!__syncthreads_or(task != T_NONE)) break;
+        STAMP(0);
 
-        // ---- T-phase: enqueue, grouped REGEN | DIFF | SPEC
-        const int* cnt = counters + 3 * parity;
-        const int n_regen = cnt[0], n_diff = cnt[1], n_spec = cnt[2];
+        // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
+        int* cnt = counters + 2 * parity;
+        const bool front = task == T_REGEN || task == T_DIFF;
+        const unsigned long long mf = __ballot(front);
+        const unsigned long long mbk = __ballot(task == T_SPEC);
+        int base_f = 0, base_b = 0;
+        if (lane == 0) {
+            if (mf) base_f = atomicAdd(&cnt[0], __popcll(mf));
+            if (mbk) base_b = atomicAdd(&cnt[1], __popcll(mbk));
+        }
+        base_f = __builtin_amdgcn_readfirstlane(base_f);
+        base_b = __builtin_amdgcn_readfirstlane(base_b);
         int slot = -1;
-        if (task == T_REGEN) slot = my_off;
-        if (task == T_DIFF) slot = n_regen + my_off;
-        if (task == T_SPEC) slot = n_regen + n_diff + my_off;
+        if (front) slot = base_f + lanes_below(mf);
+        if (task == T_SPEC) slot = BLOCK - 1 - (base_b + lanes_below(mbk));
         if (slot >= 0) {
             const f3 nrm = task == T_REGEN ? px.d0 : hn;
             SLOT(0, slot) = nrm.x;
@@ -888,25 +813,24 @@ rt_render_sorted_kernel(rt_kparams K) {
             SLOT(3, slot) = d.x;
             SLOT(4, slot) = d.y;
             SLOT(5, slot) = d.z;
-            SLOT(6, slot) = __uint_as_float(task == T_REGEN ? cand : (unsigned)hid);
+            SLOT(6, slot) = __int_as_float(task == T_REGEN ? -1 : hid);
             SLOT(7, slot) = __uint_as_float(px.rs.d);
             SLOT(8, slot) = __uint_as_float(px.rs.v0);
             SLOT(9, slot) = __uint_as_float(px.rs.v1);
             SLOT(10, slot) = __uint_as_float(px.rs.v2);
             SLOT(11, slot) = __uint_as_float(px.rs.v3);
             SLOT(12, slot) = __uint_as_float(px.rs.v4);
-            SLOT(13, slot) = hP.x;  // origin of the bounce ray
-            SLOT(14, slot) = hP.y;
-            SLOT(15, slot) = hP.z;
         }
+        STAMP(1);
         __syncthreads();
+        STAMP(2);
 
-        // ---- T-phase: execute slot `tid`: the new direction AND its closest hit
+        // ---- T-phase: execute slot `tid`
         {
-            const int kind = tid < n_regen ? T_REGEN
-                             : tid < n_regen + n_diff ? T_DIFF
-                             : tid < n_regen + n_diff + n_spec ? T_SPEC : T_NONE;
-            if (kind != T_NONE) {
+            const int nf = cnt[0], nb = cnt[1];
+            const bool do_front = tid < nf;
+            const bool do_spec = tid >= BLOCK - nb;
+            if (do_front || do_spec) {
                 Xorwow rs;
                 rs.d = __float_as_uint(SLOT(7, tid));
                 rs.v0 = __float_as_uint(SLOT(8, tid));
@@ -915,32 +839,18 @@ rt_render_sorted_kernel(rt_kparams K) {
                 rs.v3 = __float_as_uint(SLOT(11, tid));
                 rs.v4 = __float_as_uint(SLOT(12, tid));
                 const f3 nrm = mk(SLOT(0, tid), SLOT(1, tid), SLOT(2, tid));
-                const unsigned code = __float_as_uint(SLOT(6, tid));
+                const int code = __float_as_int(SLOT(6, tid));
                 f3 r;
-                float t;
-                int id;
-                if (kind == T_SPEC) {
+                if (do_front) {
+                    r = random_direction(rs, nrm);
+                    if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
+                } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
                     float kspec;
                     r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
-                    SLOT(5, tid) = kspec;
-                } else {
-                    r = random_direction(rs, nrm);
+                    SLOT(3, tid) = kspec;
                 }
-                if (kind == T_REGEN) {
-                    r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
-                    if (K.cull && r.x == r.x && r.y == r.y && r.z == r.z)
-                        closest_hit_masked(K, cam, r, code, t, id);  // primary hit, candidates only
-                    else
-                        closest_hit(K, cam, r, t, id);
-                } else {
-                    // the bounce ray's closest hit (tested even at the depth
-                    // limit, where the owner discards it: no RNG is consumed)
-                    closest_hit(K, mk(SLOT(13, tid), SLOT(14, tid), SLOT(15, tid)), r, t, id);
-                }
-                SLOT(3, tid) = t;
-                SLOT(4, tid) = __int_as_float(id);
                 SLOT(0, tid) = r.x;
                 SLOT(1, tid) = r.y;
                 SLOT(2, tid) = r.z;
@@ -952,8 +862,13 @@ rt_render_sorted_kernel(rt_kparams K) {
                 SLOT(12, tid) = __uint_as_float(rs.v4);
             }
         }
+        STAMP(3);
         __syncthreads();
-        if (tid < 3) counters[3 * parity + tid] = 0;  // all reads of this parity are done
+        STAMP(4);
+        if (tid == 0) {
+            counters[2 * (parity ^ 1)] = 0;
+            counters[2 * (parity ^ 1) + 1] = 0;
+        }
         parity ^= 1;
 
         // ---- owner: take the task result back
@@ -965,18 +880,15 @@ rt_render_sorted_kernel(rt_kparams K) {
             px.rs.v2 = __float_as_uint(SLOT(10, slot));
             px.rs.v3 = __float_as_uint(SLOT(11, slot));
             px.rs.v4 = __float_as_uint(SLOT(12, slot));
-            const int done = task;
-            task = T_NONE;
-            const float t = SLOT(3, slot);
-            const int id = __float_as_int(SLOT(4, slot));
-            if (done == T_REGEN) {
+            mode = M_IDLE;
+            if (task == T_REGEN) {
                 o = cam;
                 d = r;
                 depth = 0;
-                take_hit(t, id);
+                has_ray = true;
             } else {
-                rec_code[depth * BLOCK] = done == T_SPEC ? ~hid : hid;
-                rec_k[depth * BLOCK] = done == T_SPEC ? SLOT(5, slot) : 0.0f;
+                rec_code[depth * BLOCK] = task == T_SPEC ? ~hid : hid;
+                rec_k[depth * BLOCK] = task == T_SPEC ? SLOT(3, slot) : 0.0f;
                 rec_c[depth * BLOCK] = dot(r, hn);  // cosAngle, Main.cu:264
                 depth++;
                 o = hP;
@@ -984,11 +896,36 @@ rt_render_sorted_kernel(rt_kparams K) {
                 if (depth > K.max_bounces)  // Main.cu:210
                     finish_path();
                 else
-                    take_hit(t, id);  // brdfChoice of the next bounce (Main.cu:243)
+                    has_ray = true;
             }
         }
-        my_off = count_task(parity);
+
+        STAMP(5);
+        // ---- I-phase: closest hit + brdfChoice (Main.cu:214-245)
+        if (has_ray) {
+            has_ray = false;
+            float t;
+            int id;
+            closest_hit(K, o, d, t, id);
+            if (id >= 0) {
+                const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
+                hP = add(o, scale(t, d));
+                hn = mk(h0.x, h0.y, h0.z);
+                if (h0.w != 0.0f) hn = normalize3(sub(hP, hn));  // sphere normal
+                hid = id;
+                hspec = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE;
+                mode = M_SHADE;
+            } else {
+                finish_path();
+            }
+        }
+        STAMP(6);
     }
+#ifdef RT_STAMPS
+    if ((threadIdx.x & 63) == 0 && K.stamps)
+        for (int k = 0; k < 8; k++) atomicAdd(&K.stamps[k], st_acc[k]);
+#endif
+#undef STAMP
 #undef SLOT
 }
 
@@ -1034,7 +971,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     size_t b = hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
-    if (sorted) b += (size_t)RT_SLOT_FIELDS * block * sizeof(float) + 6 * sizeof(int);
+    if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
     return b;
 }
 

@@ -54,7 +54,6 @@ struct rt_kparams {
     const float* tri;
     const float* quad;
     const float* hit;
-    const float* cull;          // n_prim x {u.xyz, cos threshold}: primary-ray candidates (null = off)
     unsigned* rng;              // 6 planes of rows*width
     float* accum;               // 3 planes of rows*width
     unsigned* rgba;             // rows*width (may be null)
