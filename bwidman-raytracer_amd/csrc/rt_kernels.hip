@@ -349,6 +349,7 @@ __device__ __forceinline__ unsigned tone_map(float ax, float ay, float az, unsig
 
 // Per-lane pixel state ------------------------------------------------------
 struct PixelState {
+    long w;         // work item (lane slot in the tiled launch order)
     long p;         // shard pixel index
     bool valid;
     Xorwow rs;
@@ -359,6 +360,9 @@ struct PixelState {
 };
 
 __device__ __forceinline__ void load_pixel(const rt_kparams& K, long npix, long p, PixelState& s) {
+#ifdef RT_SCRAMBLE
+    if (p < npix) p = (p * 7919) % npix;  // coherence experiment only
+#endif
     s.p = p;
     s.valid = p < npix;
     s.passes_left = 0;
@@ -386,6 +390,34 @@ __device__ __forceinline__ void load_pixel(const rt_kparams& K, long npix, long 
                      K.rot[6] * pix.x + K.rot[7] * pix.y + K.rot[8] * pix.z);
     s.d0 = normalize3(pr);
     s.passes_left = K.samples;
+}
+
+// Launch order: work item w -> pixel.  Items come in groups of 64 (one
+// wave) covering a tile_w x (64/tile_w) pixel tile, tiles row-major over the
+// shard; tile_w = 0 keeps the linear order (item = pixel).  Square-ish tiles
+// keep a wave's rays spatially coherent (a pixel-scrambled order costs +45 %).
+__device__ __forceinline__ long items_of(const rt_kparams& K, long npix) {
+    if (K.tile_w <= 0) return npix;
+    const int tw = K.tile_w, th = 64 / K.tile_w;
+    const long tiles_x = (K.width + tw - 1) / tw, tiles_y = (K.rows + th - 1) / th;
+    return tiles_x * tiles_y * 64;
+}
+
+__device__ __forceinline__ long item_to_pixel(const rt_kparams& K, long npix, long w) {
+    if (K.tile_w <= 0) return w < npix ? w : npix;
+    const int tw = K.tile_w, th = 64 / K.tile_w;
+    const long tiles_x = (K.width + tw - 1) / tw;
+    const long wave = w >> 6;
+    const int l = (int)(w & 63);
+    const long x = (wave % tiles_x) * tw + (l % tw);
+    const long j = (wave / tiles_x) * th + (l / tw);
+    if (x >= K.width || j >= K.rows) return npix;
+    return j * K.width + x;
+}
+
+__device__ __forceinline__ void load_item(const rt_kparams& K, long npix, long nitems, long w, PixelState& s) {
+    load_pixel(K, npix, w < nitems ? item_to_pixel(K, npix, w) : npix, s);
+    s.w = w;
 }
 
 __device__ __forceinline__ void store_pixel(const rt_kparams& K, long npix, const PixelState& s) {
@@ -497,8 +529,9 @@ rt_render_kernel(rt_kparams K) {
 
     const long npix = (long)K.rows * K.width;
     const long T = (long)gridDim.x * BLOCK;
+    const long nitems = items_of(K, npix);
     PixelState px;
-    load_pixel(K, npix, (long)blockIdx.x * BLOCK + tid, px);
+    load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     int depth = -1;  // -1: needs a camera ray for its next frame
@@ -637,7 +670,7 @@ rt_render_kernel(rt_kparams K) {
                 depth = -1;
                 if (px.passes_left == 0) {  // pixel done: write back, take the next one
                     store_pixel(K, npix, px);
-                    load_pixel(K, npix, px.p + T, px);
+                    load_item(K, npix, nitems, px.w + T, px);
                 }
             }
             STAMP(3);
@@ -732,15 +765,40 @@ rt_render_sorted_kernel(rt_kparams K) {
     float* rec_c = rec_base + 2 * levels * BLOCK + tid;
     float* slots = rec_base + 3 * levels * BLOCK;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
-    if (tid < 4) counters[tid] = 0;
+    // counters[0..3]: queue fronts/backs (2 parities); [4] next pixel of the
+    // workgroup's chunk, [5] chunk end, [6] pixel pool exhausted
+    const long npix = (long)K.rows * K.width;
+    const long nitems = items_of(K, npix);
+    if (tid < 7) counters[tid] = 0;
+    // pixel pools: K.pool (global counter, chunks of BLOCK items) or
+    // K.lane_pixels > 1 (this workgroup owns lane_pixels * BLOCK consecutive
+    // items, handed out in order as lanes finish their pixels)
+    const int lp = K.lane_pixels > 1 ? K.lane_pixels : 1;
+    const bool pooled = K.pool || lp > 1;
+    const long item0 = K.pool ? 0 : (long)blockIdx.x * BLOCK * lp;
+    if (K.pool && tid == 0) {  // first chunk of the global pixel pool
+        const int base = atomicAdd(K.pool, BLOCK);
+        counters[4] = base;
+        counters[5] = (int)min((long)base + BLOCK, nitems);
+        counters[6] = base + BLOCK >= nitems;
+    } else if (tid == 0) {
+        counters[4] = 0;
+        counters[5] = (int)min((long)BLOCK * lp, nitems - item0);
+        counters[6] = 1;
+    }
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
 
-    const long npix = (long)K.rows * K.width;
     const long T = (long)gridDim.x * BLOCK;
     PixelState px;
-    load_pixel(K, npix, (long)blockIdx.x * BLOCK + tid, px);
+    if (pooled) {
+        const int p0 = atomicAdd(&counters[4], 1);
+        load_item(K, npix, nitems, p0 < counters[5] ? item0 + p0 : nitems, px);
+    } else {
+        load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
+    }
     int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
+    bool wants = false;  // streaming: this lane finished its pixel and takes the next
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     f3 hP = o, hn = o;  // pending hit: point, normal
@@ -765,7 +823,10 @@ rt_render_sorted_kernel(rt_kparams K) {
         px.passes_left--;
         if (px.passes_left == 0) {
             store_pixel(K, npix, px);
-            load_pixel(K, npix, px.p + T, px);
+            if (pooled)
+                wants = true;  // next pixel from the pool at the next enqueue
+            else
+                load_item(K, npix, nitems, px.w + T, px);
         }
         mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
     };
@@ -787,7 +848,18 @@ rt_render_sorted_kernel(rt_kparams K) {
     while (true) {
         const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
         STAMP(7);
-        if (!__syncthreads_or(task != T_NONE)) break;
+        // a lane that wants a pixel keeps the loop alive while its chunk has
+        // pixels left or the global pool is not exhausted
+        if (!__syncthreads_or(task != T_NONE || (wants && (counters[4] < counters[5] || !counters[6])))) break;
+        if (wants) {  // streaming: take the next pixel; its first camera ray goes out
+                      // next iteration, so the RNG-state loads have an iteration to land
+            const int pn = atomicAdd(&counters[4], 1);
+            if (pn < counters[5]) {
+                load_item(K, npix, nitems, item0 + pn, px);
+                mode = M_REGEN;
+                wants = false;
+            }
+        }
         STAMP(0);
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
@@ -824,6 +896,14 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(1);
         __syncthreads();
         STAMP(2);
+        if (K.pool && tid == 0 && counters[4] >= counters[5] && !counters[6]) {
+            // refill between this iteration's acquisitions (before the barrier
+            // above) and the next ones (after the next barrier)
+            const int base = atomicAdd(K.pool, BLOCK);
+            counters[4] = base;
+            counters[5] = (int)min((long)base + BLOCK, nitems);
+            counters[6] = base + BLOCK >= nitems;
+        }
 
         // ---- T-phase: execute slot `tid`
         {
@@ -939,8 +1019,15 @@ void* kernel_ptr() {
 
 template <int BLOCK, bool HIT_LDS, bool SORTED>
 hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
-    const long npix = (long)K.rows * K.width;
-    long grid = (npix + BLOCK - 1) / BLOCK;
+    long nitems = (long)K.rows * K.width;
+    if (K.tile_w > 0) {
+        const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
+        nitems = tiles_x * tiles_y * 64;
+    }
+    long per_group = BLOCK;
+    if (SORTED && K.lane_pixels > 1 && !K.pool) per_group = (long)BLOCK * K.lane_pixels;
+    long grid = (nitems + per_group - 1) / per_group;
+    if (SORTED && K.pool && grid_mult <= 0) grid_mult = 1;  // streaming needs a resident grid only
     if (grid_mult > 0) {  // persistent: grid_mult x resident workgroups per CU x CUs
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED>(), BLOCK, lds) ==
@@ -971,7 +1058,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     size_t b = hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
-    if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
+    if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);
     return b;
 }
 
