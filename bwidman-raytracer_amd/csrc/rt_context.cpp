@@ -84,10 +84,7 @@ struct rt_context {
     // shard state
     int width = 0, height = 0, row_offset = 0, row_stride = 1, rows = 0;
     DevBuf rng, accum, rgba;
-    DevBuf pool;  // pixel-pool counter of the streaming sorted kernel
-    bool stream_pixels = false;  // BWRT_STREAM=1
-    int tile_w = 0;              // BWRT_TILE: wave tile width (0 = linear pixel order)
-    int lane_pixels = 1;         // BWRT_LANE_PIXELS: per-workgroup pixel pool size / lanes
+    int tile_w = 16;             // BWRT_TILE: wave tile width (16 x 4 pixel waves; 0 = linear order)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
 };
@@ -217,11 +214,9 @@ int rt_create(int device, rt_context** out) {
         c->num_cus = prop.multiProcessorCount;
     if (const char* gm = std::getenv("BWRT_GRID_MULT")) c->grid_mult = std::atoi(gm);
     if (const char* kk = std::getenv("BWRT_KERNEL")) c->simple = std::strcmp(kk, "simple") == 0;
-    if (const char* sp = std::getenv("BWRT_STREAM")) c->stream_pixels = std::atoi(sp) != 0;
-    if (const char* lpx = std::getenv("BWRT_LANE_PIXELS")) c->lane_pixels = std::max(1, std::atoi(lpx));
     if (const char* tw = std::getenv("BWRT_TILE")) {
         const int t = std::atoi(tw);
-        if (t >= 1 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
+        if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
     }
     *out = c;
     return RT_OK;
@@ -236,7 +231,6 @@ void rt_destroy(rt_context* c) {
     free_buf(c->rng);
     free_buf(c->accum);
     free_buf(c->rgba);
-    free_buf(c->pool);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -441,14 +435,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
             (void)hipMemsetAsync(stamps, 0, 8 * sizeof(unsigned long long), s);
         K.stamps = stamps;
     }
-    if (c->stream_pixels && !c->simple) {
-        int rc = ensure_buf(c, c->pool, sizeof(int));
-        if (rc) return rc;
-        HIP_TRY(c, hipMemsetAsync(c->pool.p, 0, sizeof(int), s));
-        K.pool = (int*)c->pool.p;
-    }
     K.tile_w = c->tile_w;
-    K.lane_pixels = c->lane_pixels;
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, s);
     if (stamps) {

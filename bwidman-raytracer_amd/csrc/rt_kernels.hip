@@ -765,40 +765,17 @@ rt_render_sorted_kernel(rt_kparams K) {
     float* rec_c = rec_base + 2 * levels * BLOCK + tid;
     float* slots = rec_base + 3 * levels * BLOCK;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
-    // counters[0..3]: queue fronts/backs (2 parities); [4] next pixel of the
-    // workgroup's chunk, [5] chunk end, [6] pixel pool exhausted
+    // counters[0..3]: queue fronts/backs (2 parities)
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
-    if (tid < 7) counters[tid] = 0;
-    // pixel pools: K.pool (global counter, chunks of BLOCK items) or
-    // K.lane_pixels > 1 (this workgroup owns lane_pixels * BLOCK consecutive
-    // items, handed out in order as lanes finish their pixels)
-    const int lp = K.lane_pixels > 1 ? K.lane_pixels : 1;
-    const bool pooled = K.pool || lp > 1;
-    const long item0 = K.pool ? 0 : (long)blockIdx.x * BLOCK * lp;
-    if (K.pool && tid == 0) {  // first chunk of the global pixel pool
-        const int base = atomicAdd(K.pool, BLOCK);
-        counters[4] = base;
-        counters[5] = (int)min((long)base + BLOCK, nitems);
-        counters[6] = base + BLOCK >= nitems;
-    } else if (tid == 0) {
-        counters[4] = 0;
-        counters[5] = (int)min((long)BLOCK * lp, nitems - item0);
-        counters[6] = 1;
-    }
+    if (tid < 4) counters[tid] = 0;
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
 
     const long T = (long)gridDim.x * BLOCK;
     PixelState px;
-    if (pooled) {
-        const int p0 = atomicAdd(&counters[4], 1);
-        load_item(K, npix, nitems, p0 < counters[5] ? item0 + p0 : nitems, px);
-    } else {
-        load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
-    }
+    load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
     int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
-    bool wants = false;  // streaming: this lane finished its pixel and takes the next
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     f3 hP = o, hn = o;  // pending hit: point, normal
@@ -823,10 +800,7 @@ rt_render_sorted_kernel(rt_kparams K) {
         px.passes_left--;
         if (px.passes_left == 0) {
             store_pixel(K, npix, px);
-            if (pooled)
-                wants = true;  // next pixel from the pool at the next enqueue
-            else
-                load_item(K, npix, nitems, px.w + T, px);
+            load_item(K, npix, nitems, px.w + T, px);
         }
         mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
     };
@@ -848,18 +822,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     while (true) {
         const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
         STAMP(7);
-        // a lane that wants a pixel keeps the loop alive while its chunk has
-        // pixels left or the global pool is not exhausted
-        if (!__syncthreads_or(task != T_NONE || (wants && (counters[4] < counters[5] || !counters[6])))) break;
-        if (wants) {  // streaming: take the next pixel; its first camera ray goes out
-                      // next iteration, so the RNG-state loads have an iteration to land
-            const int pn = atomicAdd(&counters[4], 1);
-            if (pn < counters[5]) {
-                load_item(K, npix, nitems, item0 + pn, px);
-                mode = M_REGEN;
-                wants = false;
-            }
-        }
+        if (!__syncthreads_or(task != T_NONE)) break;
         STAMP(0);
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
@@ -896,14 +859,6 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(1);
         __syncthreads();
         STAMP(2);
-        if (K.pool && tid == 0 && counters[4] >= counters[5] && !counters[6]) {
-            // refill between this iteration's acquisitions (before the barrier
-            // above) and the next ones (after the next barrier)
-            const int base = atomicAdd(K.pool, BLOCK);
-            counters[4] = base;
-            counters[5] = (int)min((long)base + BLOCK, nitems);
-            counters[6] = base + BLOCK >= nitems;
-        }
 
         // ---- T-phase: execute slot `tid`
         {
@@ -1024,10 +979,7 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
         const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
         nitems = tiles_x * tiles_y * 64;
     }
-    long per_group = BLOCK;
-    if (SORTED && K.lane_pixels > 1 && !K.pool) per_group = (long)BLOCK * K.lane_pixels;
-    long grid = (nitems + per_group - 1) / per_group;
-    if (SORTED && K.pool && grid_mult <= 0) grid_mult = 1;  // streaming needs a resident grid only
+    long grid = (nitems + BLOCK - 1) / BLOCK;  // streaming needs a resident grid only
     if (grid_mult > 0) {  // persistent: grid_mult x resident workgroups per CU x CUs
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED>(), BLOCK, lds) ==
@@ -1058,7 +1010,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     size_t b = hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
-    if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);
+    if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
     return b;
 }
 

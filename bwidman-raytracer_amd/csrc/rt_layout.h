@@ -58,7 +58,5 @@ struct rt_kparams {
     float* accum;               // 3 planes of rows*width
     unsigned* rgba;             // rows*width (may be null)
     unsigned long long* stamps; // diagnostic builds (-DRT_STAMPS) only: per-phase cycle sums
-    int* pool;                  // sorted kernel: global pixel counter (null = one pixel per lane)
     int tile_w;                 // wave tile width in pixels (1..64, power of 2); 0 = linear order
-    int lane_pixels;            // sorted kernel: pixels per lane handed out from a per-workgroup pool
 };
