@@ -3,6 +3,14 @@ import sys
 
 import pytest
 
+# Load PyTorch (and its HIP runtime) before libbwrt.so, so that both share one
+# HIP runtime (same soname) and torch streams / tensors can be passed to the
+# C ABI (bench.py does the same).
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (REPO, os.path.join(REPO, "bwidman-raytracer_amd"), os.path.join(REPO, "oracle")):
     if p not in sys.path:

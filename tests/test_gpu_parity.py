@@ -200,3 +200,51 @@ def test_converges_to_reference_png(gpu):
         # the GPU is bit-exact with the oracle, so it reproduces the oracle's MAE
         assert abs(mae - json.load(open(ref))["block_mean_mae_lsb"]) < 1e-6
     assert mae <= 1.5, mae
+
+
+def test_config4_07_4k_max_size(gpu, oracle):
+    """BASELINE config 4's per-GPU work at its full size on one GPU: 07 scene,
+    3840x2160 (jitter scale 0.003), 16 spp, 6 bounces — bit-exact."""
+    img, st = run_pair(gpu, oracle, scenes.scene_07(), 3840, 2160, 16, 6)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+def test_config4_shard_of_8(gpu, oracle):
+    """One of the 8 interleaved-row shards of config 4 (rows 5, 13, 21, ...)."""
+    img, st = run_pair(gpu, oracle, scenes.scene_07(), 3840, 2160, 16, 6, row_offset=5, row_stride=8)
+    assert np.array_equal(img, st.rgba)
+
+
+def test_deinterleave_kernel(gpu):
+    """rt_deinterleave_rows_device (the multi-GPU gather epilogue) on device
+    buffers: gathered [shards][rows_per_shard][W] -> image [H][W]."""
+    import torch
+    from bwrt.dist import ShardPlan, deinterleave_reference
+    for h, w, shards in [(1080, 1920, 8), (55, 33, 2), (7, 5, 3)]:
+        plan = ShardPlan(h, shards, 0)
+        g = torch.randint(0, 2**31 - 1, (shards * plan.rows_per_shard * w,), dtype=torch.int32, device="cuda")
+        out = torch.empty(h * w, dtype=torch.int32, device="cuda")
+        gpu.deinterleave_device(g.data_ptr(), out.data_ptr(), w, h, shards, plan.rows_per_shard,
+                                torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want = deinterleave_reference(g.cpu().numpy().reshape(shards, plan.rows_per_shard, w, 1), plan, w)
+        assert np.array_equal(out.cpu().numpy().reshape(h, w), want[..., 0])
+
+
+def test_render_device_into_torch_buffer(gpu, oracle):
+    """rt_render_device into a torch-allocated device buffer on a torch stream
+    (the bench / multi-GPU path) equals the host-buffer render."""
+    import torch
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    w, h = 256, 144
+    gpu.init_rand(w, h)
+    buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.Stream()
+    gpu.render_device(gpu.params(w, h, 3, 4, first_frame=1), buf.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    img = buf.cpu().numpy().view(np.uint8).reshape(h, w, 4)
+    st = oracle.render_image(s, w, h, 3, 4)
+    assert np.array_equal(img, st.rgba)
+    assert gpu.last_kernel_ms() > 0
