@@ -50,6 +50,15 @@ def parse():
     return ap.parse_args()
 
 
+SCENE_NAMES = {"01": "01_red_circle", "04": "04_path_tracing", "07": "07_specular_BRDF", "stress": "stress_10k"}
+SCENE_DATA = {
+    "01": "reference scene 01 (one red sphere)",
+    "04": "reference scene 04 (07 spheres 0,1,4,5 + floor)",
+    "07": "reference scene 07 (Main.cu:39-67)",
+    "stress": "stress scene (10,000 triangles + 256 spheres + floor, xorshift32 seed, bwrt/scenes.py)",
+}
+
+
 def cpu_baseline(scene_key, w, h, spp, mb, threads):
     """The oracle (C restatement, OpenMP over rows) on the host cores: the
     reported CPU baseline ("port"), never the measured product."""
@@ -161,7 +170,7 @@ def main():
         workload_key = f"{scene_key}-{W}x{H}-{SPP}spp-{MB}b-rows{world}"
         traffic = load_traffic(args.traffic_json, workload_key)
         out = {
-            "metric": "Msamples/sec (W*H*spp*bounces/t), 1920x1080 8spp 4-bounce, 07_specular_BRDF",
+            "metric": f"Msamples/sec (W*H*spp*bounces/t), {W}x{H} {SPP}spp {MB}-bounce, {SCENE_NAMES[scene_key]}",
             "value": round(value, 2),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -172,7 +181,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: reference scene 07 (Main.cu:39-67), per-pixel RNG seeded y*W+x",
+            "data": f"synthetic: {SCENE_DATA[scene_key]}, per-pixel RNG seeded y*W+x",
             "config": {"workload": f"07_specular_BRDF {W}x{H} {SPP}spp {MB}-bounce (BASELINE configs[2])"
                        if args.config == "c3" else f"{args.config}: scene {scene_key} {W}x{H} {SPP}spp {MB}-bounce",
                        "scene": scene_key, "width": W, "height": H, "spp": SPP, "max_bounces": MB,

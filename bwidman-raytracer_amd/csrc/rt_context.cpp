@@ -78,7 +78,8 @@ struct rt_context {
     bool has_scene = false;
     rt_camera camera{};
     int n_sph = 0, n_pln = 0, n_tri = 0, n_quad = 0;
-    DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table
+    DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table | bvh nodes | bvh prims
+    size_t off_bvh = 0, off_bvh_prims = 0;  // in floats; 0 = no BVH
     size_t off_pln = 0, off_tri = 0, off_quad = 0, off_hit = 0;  // in floats
 
     // shard state
@@ -173,6 +174,87 @@ void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_
     h[3] = 0.0f;
     put_material(h, m);
 }
+
+// ---- BVH over spheres / triangles / quads (large scenes) -------------------
+// Depth-first node array with miss links (rt_layout.h); median split on the
+// widest centroid axis, <= 4 primitives per leaf.  Boxes are inflated by
+// 1e-3 + 1e-4 * |coordinate| — orders of magnitude beyond the rounding of
+// the reference's hit tests — so every hit the reference can accept lies
+// inside its leaf's box.
+struct BvhItem {
+    float lo[3], hi[3], c[3];
+    int id;
+};
+
+struct BvhBuilder {
+    std::vector<BvhItem> items;
+    std::vector<float> nodes;  // 8 floats per node
+    std::vector<int> prims;
+
+    static float inflate(float v) { return 1e-3f + 1e-4f * std::fabs(v); }
+
+    int build(int b, int e) {
+        const int node = (int)(nodes.size() / 8);
+        nodes.resize(nodes.size() + 8);
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = b; i < e; i++)
+            for (int a = 0; a < 3; a++) {
+                lo[a] = std::min(lo[a], items[i].lo[a]);
+                hi[a] = std::max(hi[a], items[i].hi[a]);
+                clo[a] = std::min(clo[a], items[i].c[a]);
+                chi[a] = std::max(chi[a], items[i].c[a]);
+            }
+        int leaf = -1;
+        if (e - b <= 4) {
+            leaf = ((e - b) << 24) | (int)prims.size();
+            for (int i = b; i < e; i++) prims.push_back(items[i].id);
+        } else {
+            int axis = 0;
+            for (int a = 1; a < 3; a++)
+                if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+            const int mid = (b + e) / 2;
+            std::nth_element(items.begin() + b, items.begin() + mid, items.begin() + e,
+                             [axis](const BvhItem& x, const BvhItem& y) {
+                                 return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.id < y.id);
+                             });
+            build(b, mid);
+            build(mid, e);
+        }
+        float* n = &nodes[8 * (size_t)node];
+        for (int a = 0; a < 3; a++) {
+            n[a] = lo[a];
+            n[4 + a] = hi[a];
+        }
+        const int end = (int)(nodes.size() / 8);  // first node after this subtree
+        int miss = -2;                             // patched below
+        std::memcpy(&n[3], &miss, 4);
+        std::memcpy(&n[7], &leaf, 4);
+        subtree_end.resize(end);
+        subtree_end[node] = end;
+        return node;
+    }
+    std::vector<int> subtree_end;
+
+    void finish() {
+        const int total = (int)(nodes.size() / 8);
+        for (int i = 0; i < total; i++) {
+            const int miss = subtree_end[i] < total ? subtree_end[i] : -1;
+            std::memcpy(&nodes[8 * (size_t)i + 3], &miss, 4);
+        }
+    }
+
+    void add(int id, const float* lo, const float* hi) {
+        BvhItem it;
+        for (int a = 0; a < 3; a++) {
+            it.lo[a] = lo[a] - inflate(lo[a]);
+            it.hi[a] = hi[a] + inflate(hi[a]);
+            it.c[a] = 0.5f * (lo[a] + hi[a]);
+        }
+        it.id = id;
+        items.push_back(it);
+    }
+};
 
 }  // namespace
 
@@ -290,10 +372,48 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     for (int i = 0; i < nq; i++, id++)
         compile_polygon(h.data() + off_quad + (size_t)i * RT_QUAD_FLOATS, hit + (size_t)id * RT_HIT_FLOATS,
                         s->quads[i].vertices, 4, s->quads[i].mat);
-    int rc = ensure_buf(c, c->scene_buf, total * sizeof(float));
+    // BVH for large scenes (BWRT_BVH_MIN primitives, default 64)
+    size_t off_bvh = 0, off_bvh_prims = 0;
+    {
+        int bvh_min = 64;
+        if (const char* e = std::getenv("BWRT_BVH_MIN")) bvh_min = std::atoi(e);
+        const int nb = ns + nt + nq;
+        if (nb > 0 && nb >= bvh_min) {
+            BvhBuilder B;
+            B.items.reserve(nb);
+            for (int i = 0; i < ns; i++) {
+                const rt_sphere& sp = s->spheres[i];
+                const float r = std::fabs(sp.radius);
+                const float lo[3] = {sp.position.x - r, sp.position.y - r, sp.position.z - r};
+                const float hi[3] = {sp.position.x + r, sp.position.y + r, sp.position.z + r};
+                B.add(i, lo, hi);
+            }
+            auto poly = [&](int id, const rt_vec3* v, int nv) {
+                float lo[3] = {v[0].x, v[0].y, v[0].z}, hi[3] = {v[0].x, v[0].y, v[0].z};
+                for (int k = 1; k < nv; k++) {
+                    const float p[3] = {v[k].x, v[k].y, v[k].z};
+                    for (int a = 0; a < 3; a++) {
+                        lo[a] = std::min(lo[a], p[a]);
+                        hi[a] = std::max(hi[a], p[a]);
+                    }
+                }
+                B.add(id, lo, hi);
+            };
+            for (int i = 0; i < nt; i++) poly(ns + np + i, s->triangles[i].vertices, 3);
+            for (int i = 0; i < nq; i++) poly(ns + np + nt + i, s->quads[i].vertices, 4);
+            B.build(0, nb);
+            B.finish();
+            off_bvh = (total + 3) & ~(size_t)3;
+            off_bvh_prims = off_bvh + B.nodes.size();
+            h.resize(off_bvh_prims + B.prims.size() + 4, 0.0f);
+            std::memcpy(h.data() + off_bvh, B.nodes.data(), B.nodes.size() * sizeof(float));
+            std::memcpy(h.data() + off_bvh_prims, B.prims.data(), B.prims.size() * sizeof(int));
+        }
+    }
+    const size_t bytes = h.size() * sizeof(float);
+    int rc = ensure_buf(c, c->scene_buf, bytes);
     if (rc) return rc;
-    HIP_TRY(c, hipMemcpyAsync(c->scene_buf.p, h.data(), total * sizeof(float), hipMemcpyHostToDevice,
-                              c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->scene_buf.p, h.data(), bytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->n_sph = ns;
     c->n_pln = np;
@@ -303,6 +423,8 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     c->off_tri = off_tri;
     c->off_quad = off_quad;
     c->off_hit = off_hit;
+    c->off_bvh = off_bvh;
+    c->off_bvh_prims = off_bvh_prims;
     c->camera = s->camera;
     c->has_scene = true;
     c->frame = 1;
@@ -423,6 +545,8 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.tri = base + c->off_tri;
     K.quad = base + c->off_quad;
     K.hit = base + c->off_hit;
+    K.bvh_nodes = c->off_bvh ? base + c->off_bvh : nullptr;
+    K.bvh_prims = c->off_bvh ? reinterpret_cast<const int*>(base + c->off_bvh_prims) : nullptr;
     K.rng = (unsigned*)c->rng.p;
     K.accum = (float*)c->accum.p;
     return RT_OK;

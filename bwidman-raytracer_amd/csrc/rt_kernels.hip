@@ -272,7 +272,7 @@ __device__ __forceinline__ void polygon_test(const __attribute__((address_space(
 typedef const __attribute__((address_space(4))) float* cfloat_ptr;
 __device__ __forceinline__ cfloat_ptr as_const(const float* p) { return (cfloat_ptr)p; }
 
-__device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
+__device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
     const float a = dot(d, d);
     const float a4 = 4.0f * a;
     const float a2 = 2.0f * a;
@@ -319,6 +319,138 @@ __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, flo
         if (i < K.n_tri) polygon_test(as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, best_t, best_id);
         if (i < K.n_quad) polygon_test(as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, best_t, best_id);
     }
+}
+
+// ---- BVH closest hit (large scenes, e.g. the 10k-triangle stress scene) ----
+// Exactness: every primitive is tested with the reference's own arithmetic
+// (the same code as closest_hit_brute) and accepted when
+//   t > nearZero  and  (t < best  or  (t == best and key > best_key)),
+// so the winner is the minimum distance with ties resolved to the primitive
+// the reference tests last (RT_KEY order) — exactly what the reference's
+// running `t > closest` test in interleaved order returns, whatever order
+// the BVH visits primitives in.  This needs finite rays (all t finite, never
+// NaN); a ray with a NaN/inf component takes the brute-force loop, which
+// reproduces the reference's NaN acceptance behaviour.  Node boxes are
+// inflated far beyond float rounding and the slab test only ever prunes
+// with margins, so no primitive the reference could hit is skipped.
+__device__ __forceinline__ bool key_accept(float t, int key, float best_t, int best_key) {
+    return !(t <= RT_NEAR_ZERO) && (t < best_t || (t == best_t && key > best_key));
+}
+
+__device__ __forceinline__ void prim_test(const rt_kparams& K, int id, f3 o, f3 d, float a2, float a4, float& best_t,
+                                          int& best_id, int& best_key) {
+    const int ns = K.n_sph, tri_base = K.n_sph + K.n_pln, quad_base = tri_base + K.n_tri;
+    if (id < ns) {  // Intersection.cuh:15-62
+        const float4 s = *reinterpret_cast<const float4*>(K.sph + RT_SPH_FLOATS * id);
+        const f3 xp = mk(o.x - s.x, o.y - s.y, o.z - s.z);
+        const float b = 2.0f * dot(xp, d);
+        const float c = dot(xp, xp) - s.w;
+        const float disc = b * b - a4 * c;
+        if (!(disc < 0.0f) && !(b >= 0.0f)) {
+            const float t = (-b - sqrtf(disc)) / a2;
+            const int key = RT_KEY(0, id);
+            if (key_accept(t, key, best_t, best_key)) {
+                best_t = t;
+                best_id = id;
+                best_key = key;
+            }
+        }
+        return;
+    }
+    const bool is_tri = id < quad_base;
+    const int idx = is_tri ? id - tri_base : id - quad_base;
+    const float* q = is_tri ? K.tri + RT_TRI_FLOATS * idx : K.quad + RT_QUAD_FLOATS * idx;
+    const int nv = is_tri ? 3 : 4;
+    const float4 nq = *reinterpret_cast<const float4*>(q);
+    const float nd = nq.x * d.x + nq.y * d.y + nq.z * d.z;
+    if (fabsf(nd) < RT_NEAR_ZERO) return;
+    const float t = -((nq.x * o.x + nq.y * o.y + nq.z * o.z) + nq.w) / nd;
+    const int key = RT_KEY(is_tri ? 2 : 3, idx);
+    if (!key_accept(t, key, best_t, best_key)) return;
+    const f3 P = add(o, scale(t, d));
+    const float4 e0 = *reinterpret_cast<const float4*>(q + 4);   // v0.xyz in0.x
+    const float4 e1 = *reinterpret_cast<const float4*>(q + 8);   // in0.yz v1.xy
+    const float4 e2 = *reinterpret_cast<const float4*>(q + 12);  // v1.z in1.xyz
+    const float4 e3 = *reinterpret_cast<const float4*>(q + 16);  // v2.xyz in2.x
+    const float4 e4 = *reinterpret_cast<const float4*>(q + 20);  // in2.yz (v3.xy)
+    bool inside = !(dot(mk(e0.w, e1.x, e1.y), sub(P, mk(e0.x, e0.y, e0.z))) < 0.0f) &&
+                  !(dot(mk(e2.y, e2.z, e2.w), sub(P, mk(e1.z, e1.w, e2.x))) < 0.0f) &&
+                  !(dot(mk(e3.w, e4.x, e4.y), sub(P, mk(e3.x, e3.y, e3.z))) < 0.0f);
+    if (nv == 4 && inside) {
+        const float4 e5 = *reinterpret_cast<const float4*>(q + 24);  // v3.z in3.xyz
+        inside = !(dot(mk(e5.y, e5.z, e5.w), sub(P, mk(e4.z, e4.w, e5.x))) < 0.0f);
+    }
+    if (inside) {
+        best_t = t;
+        best_id = id;
+        best_key = key;
+    }
+}
+
+__device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
+    const bool finite = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
+                        fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
+    if (!finite) {  // NaN/inf rays: the reference's interleaved loop
+        closest_hit_brute(K, o, d, best_t, best_id);
+        return;
+    }
+    const float a = dot(d, d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    best_t = INFINITY;
+    best_id = -1;
+    int best_key = -1;
+    for (int i = 0; i < K.n_pln; i++) {  // planes are unbounded: always tested
+        const cfloat_ptr q = as_const(K.pln) + RT_PLN_FLOATS * i;
+        const float nd = q[0] * d.x + q[1] * d.y + q[2] * d.z;
+        if (!(fabsf(nd) < RT_NEAR_ZERO)) {
+            const float t = -((q[0] * o.x + q[1] * o.y + q[2] * o.z) + q[3]) / nd;
+            const int key = RT_KEY(1, i);
+            if (key_accept(t, key, best_t, best_key)) {
+                best_t = t;
+                best_id = K.n_sph + i;
+                best_key = key;
+            }
+        }
+    }
+    // slab test with a direction clamped away from 0 (sign kept): a
+    // conservative stand-in for the axis-parallel case
+    const float tiny = 1e-20f;
+    const f3 dc = mk(fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x, fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y,
+                     fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z);
+    const f3 inv = mk(1.0f / dc.x, 1.0f / dc.y, 1.0f / dc.z);
+    int node = 0;
+    while (node >= 0) {
+        const float4 lo = *reinterpret_cast<const float4*>(K.bvh_nodes + 8 * node);
+        const float4 hi = *reinterpret_cast<const float4*>(K.bvh_nodes + 8 * node + 4);
+        const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
+        const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
+        const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+        const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+        const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+        // margins: 1e-5 relative + 1e-6 absolute on the interval, and prune
+        // against the current closest distance only beyond the same margin
+        const bool hit = tmin <= tmax * (1.0f + 1e-5f) + 1e-6f && tmin <= best_t * (1.0f + 1e-5f) + 1e-5f;
+        const int miss = __float_as_int(lo.w);
+        const int leaf = __float_as_int(hi.w);
+        if (!hit) {
+            node = miss;
+        } else if (leaf < 0) {
+            node = node + 1;
+        } else {
+            const int first = leaf & 0xffffff, count = leaf >> 24;
+            for (int k = 0; k < count; k++) prim_test(K, K.bvh_prims[first + k], o, d, a2, a4, best_t, best_id, best_key);
+            node = miss;
+        }
+    }
+}
+
+template <bool BVH>
+__device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
+    if (BVH)
+        closest_hit_bvh(K, o, d, best_t, best_id);
+    else
+        closest_hit_brute(K, o, d, best_t, best_id);
 }
 
 __device__ __forceinline__ unsigned to_u8(float v) {
@@ -509,7 +641,7 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 #define RT_WAVES_PER_EU 1
 #endif
 
-template <int BLOCK, bool HIT_LDS>
+template <int BLOCK, bool HIT_LDS, bool BVH>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
 rt_render_kernel(rt_kparams K) {
     extern __shared__ float smem[];
@@ -571,7 +703,7 @@ rt_render_kernel(rt_kparams K) {
             // (2) closest hit (Main.cu:214-234)
             float t;
             int id;
-            closest_hit(K, o, d, t, id);
+            closest_hit<BVH>(K, o, d, t, id);
             STAMP(1);
 
             bool finished = true;
@@ -743,7 +875,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 //
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
-template <int BLOCK, bool HIT_LDS>
+template <int BLOCK, bool HIT_LDS, bool BVH>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
     enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
@@ -941,7 +1073,7 @@ rt_render_sorted_kernel(rt_kparams K) {
             has_ray = false;
             float t;
             int id;
-            closest_hit(K, o, d, t, id);
+            closest_hit<BVH>(K, o, d, t, id);
             if (id >= 0) {
                 const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
                 hP = add(o, scale(t, d));
@@ -966,13 +1098,13 @@ rt_render_sorted_kernel(rt_kparams K) {
 
 // ---- launchers (host side) ------------------------------------------------
 namespace {
-template <int BLOCK, bool HIT_LDS, bool SORTED>
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH>
 void* kernel_ptr() {
-    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS>)
-                  : reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS>);
+    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH>)
+                  : reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
 }
 
-template <int BLOCK, bool HIT_LDS, bool SORTED>
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH>
 hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
     long nitems = (long)K.rows * K.width;
     if (K.tile_w > 0) {
@@ -982,7 +1114,7 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
     long grid = (nitems + BLOCK - 1) / BLOCK;  // streaming needs a resident grid only
     if (grid_mult > 0) {  // persistent: grid_mult x resident workgroups per CU x CUs
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED>(), BLOCK, lds) ==
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH>(), BLOCK, lds) ==
                 hipSuccess &&
             per_cu > 0) {
             const long cap = (long)per_cu * num_cus * grid_mult;
@@ -991,16 +1123,19 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
     }
     if (grid < 1) grid = 1;
     if (SORTED)
-        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream,
+                           K);
     else
-        hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+        hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
     return hipGetLastError();
 }
 
 template <int BLOCK, bool SORTED>
 hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s) {
-    return hit_lds ? launch_render<BLOCK, true, SORTED>(K, lds, grid_mult, num_cus, s)
-                   : launch_render<BLOCK, false, SORTED>(K, lds, grid_mult, num_cus, s);
+    if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
+        return launch_render<BLOCK, false, SORTED, true>(K, lds, grid_mult, num_cus, s);
+    return hit_lds ? launch_render<BLOCK, true, SORTED, false>(K, lds, grid_mult, num_cus, s)
+                   : launch_render<BLOCK, false, SORTED, false>(K, lds, grid_mult, num_cus, s);
 }
 }  // namespace
 
@@ -1020,7 +1155,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 // grid_mult x resident workgroups per CU (persistent lanes).
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, hipStream_t stream) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
-    const bool hit_lds = (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
+    const bool hit_lds = !K.bvh_nodes && (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
     const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 49152;
     const int block = small_block ? 64 : 256;
     const size_t lds = rt_render_lds_bytes(K, block, hit_lds, !simple);

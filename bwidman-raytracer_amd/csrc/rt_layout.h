@@ -59,4 +59,16 @@ struct rt_kparams {
     unsigned* rgba;             // rows*width (may be null)
     unsigned long long* stamps; // diagnostic builds (-DRT_STAMPS) only: per-phase cycle sums
     int tile_w;                 // wave tile width in pixels (1..64, power of 2); 0 = linear order
+    // bounding-volume hierarchy over spheres/triangles/quads (large scenes;
+    // null = brute-force loop).  nodes: 8 floats {bmin.xyz, miss, bmax.xyz,
+    // leaf}, depth-first order (first child = node + 1), miss = next node
+    // when the subtree is skipped (-1 = done), leaf = -1 (internal) or
+    // (count << 24) | first index into bvh_prims (global primitive ids).
+    const float* bvh_nodes;
+    const int* bvh_prims;
 };
+
+// Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,
+// quad i, then i+1): a primitive's key; among equal distances the reference
+// keeps the LAST tested primitive, i.e. the largest key.
+#define RT_KEY(kind, i) ((i) * 4 + (kind))

@@ -77,6 +77,32 @@ def test_stress_scene_small(gpu, oracle):
     same_state(gpu, st)
 
 
+def test_stress_c5_rows_bvh(gpu, oracle):
+    """Config-5 geometry (1920x1080 stress scene, 8 bounces) on 8 full-width
+    rows (y = 3 mod 135): 10,256 primitives take the BVH path; the oracle is
+    the reference's brute-force loop, so this pins the BVH's exact
+    key-ordered tie-breaking and conservative culling."""
+    img, st = run_pair(gpu, oracle, scenes.stress_scene(), 1920, 1080, 2, 8, row_offset=3, row_stride=135)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+@pytest.mark.parametrize("name,w,h,spp,mb", [("07", 320, 180, 4, 5), ("04", 320, 180, 4, 3),
+                                              ("04_box", 320, 180, 4, 5), ("01", 256, 256, 1, 1)])
+def test_bvh_forced_on_small_scenes(gpu, oracle, monkeypatch, name, w, h, spp, mb):
+    """BWRT_BVH_MIN=1 routes even the reference scenes through the BVH: their
+    shared pyramid / box edges produce exact distance ties, which the BVH must
+    resolve to the same primitive as the reference's interleaved loop."""
+    monkeypatch.setenv("BWRT_BVH_MIN", "1")
+    scene = {"07": scenes.scene_07, "04": scenes.scene_04, "04_box": scenes.scene_04_box,
+             "01": scenes.scene_01}[name]()
+    img, st = run_pair(gpu, oracle, scene, w, h, spp, mb)
+    monkeypatch.delenv("BWRT_BVH_MIN")
+    gpu.set_scene(scenes.scene_07())  # leave the session renderer on the brute-force path
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
 @pytest.mark.parametrize("w,h", [(100, 37), (1, 1), (63, 65)])
 def test_ragged_sizes(gpu, oracle, w, h):
     img, st = run_pair(gpu, oracle, scenes.scene_07(), w, h, 3, 4)
