@@ -78,6 +78,7 @@ struct rt_context {
     bool has_scene = false;
     rt_camera camera{};
     int n_sph = 0, n_pln = 0, n_tri = 0, n_quad = 0;
+    float cull_omax = 0.0f;  // polygon culling bound (rt_layout.h)
     DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table | bvh nodes | bvh prims
     size_t off_bvh = 0, off_bvh_prims = 0;  // in floats; 0 = no BVH
     size_t off_pln = 0, off_tri = 0, off_quad = 0, off_hit = 0;  // in floats
@@ -148,7 +149,56 @@ void put_material(float* h, const rt_material& m) {
 }
 
 // Triangle / quad record: {n, d, v0, in0, v1, in1, ...}; Intersection.cuh:109-127
-void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_material& m) {
+// Cull sphere of a triangle, used by polygon_test to skip the exact test for
+// rays whose LINE passes farther than Rc from the centre.  Such a ray's
+// plane hit P (as the reference computes it, with float rounding) is at
+// least Rc - R from the triangle; outside a triangle with smallest angle
+// alpha some edge function dot(in_k, P - v_k) is then below
+// -|in_k| * (Rc - R) * sin(alpha / 2), and the inflation
+//   Rc = R (1 + 2^-20) + 2^-14 * scale / (0.25 sin alpha)
+// (scale >= every coordinate of the scene and of any culled ray origin)
+// keeps that margin > 2^-14 * scale, several hundred times the rounding of
+// the reference's P = o + t d and of its edge dots (~2^-21 * scale).  So the
+// reference rejects every culled triangle.  Degenerate/skinny triangles
+// (sin alpha < 2^-10) and quads (possibly non-convex / non-planar) are never
+// culled (Rc^2 = inf).
+void cull_sphere(float* cs, const rt_vec3* verts, int nv, double scale) {
+    cs[0] = cs[1] = cs[2] = 0.0f;
+    cs[3] = INFINITY;
+    if (nv != 3) return;
+    double v[3][3];
+    for (int k = 0; k < 3; k++) {
+        v[k][0] = verts[k].x;
+        v[k][1] = verts[k].y;
+        v[k][2] = verts[k].z;
+    }
+    double c[3], r = 0.0, min_sin = 1.0;
+    for (int a = 0; a < 3; a++) c[a] = (v[0][a] + v[1][a] + v[2][a]) / 3.0;
+    for (int k = 0; k < 3; k++) {
+        double d2 = 0.0, e1[3], e2[3], l1 = 0.0, l2 = 0.0, dp = 0.0;
+        for (int a = 0; a < 3; a++) {
+            d2 += (v[k][a] - c[a]) * (v[k][a] - c[a]);
+            e1[a] = v[(k + 1) % 3][a] - v[k][a];
+            e2[a] = v[(k + 2) % 3][a] - v[k][a];
+            l1 += e1[a] * e1[a];
+            l2 += e2[a] * e2[a];
+            dp += e1[a] * e2[a];
+        }
+        r = std::max(r, std::sqrt(d2));
+        const double cosang = (l1 > 0.0 && l2 > 0.0) ? dp / std::sqrt(l1 * l2) : 1.0;
+        min_sin = std::min(min_sin, std::sqrt(std::max(0.0, 1.0 - cosang * cosang)));
+    }
+    if (!(min_sin >= 1.0 / 1024.0) || !std::isfinite(r) || !std::isfinite(scale)) return;
+    const double rc = r * (1.0 + std::ldexp(1.0, -20)) + std::ldexp(1.0, -14) * scale / (0.25 * min_sin);
+    const double rc2 = rc * rc * (1.0 + std::ldexp(1.0, -20));
+    if (!(rc2 < 1e30)) return;
+    cs[0] = (float)c[0];
+    cs[1] = (float)c[1];
+    cs[2] = (float)c[2];
+    cs[3] = (float)rc2;
+}
+
+void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_material& m, double scale) {
     V3 v[4], e[4];
     for (int k = 0; k < nv; k++) v[k] = v3(verts[k]);
     for (int k = 0; k < nv; k++) e[k] = sub(v[(k + 1) % nv], v[k]);
@@ -173,6 +223,9 @@ void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_
     h[2] = n.z;
     h[3] = 0.0f;
     put_material(h, m);
+    // cull sphere (centre, Rc^2), appended after the edge data
+    float* cs = q + (nv == 3 ? RT_TRI_CULL : RT_QUAD_CULL);
+    cull_sphere(cs, verts, nv, scale);
 }
 
 // ---- BVH over spheres / triangles / quads (large scenes) -------------------
@@ -366,12 +419,27 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
         hh[3] = 0.0f;
         put_material(hh, pl.mat);
     }
+    // scene scale for polygon culling: >= every primitive coordinate and the
+    // camera position; rays whose origin lies beyond it are never culled
+    double scale = 1.0;
+    auto grow = [&](const rt_vec3& v, double extra) {
+        scale = std::max(scale, std::max(std::fabs((double)v.x), std::max(std::fabs((double)v.y), std::fabs((double)v.z))) + extra);
+    };
+    grow(s->camera.position, 0.0);
+    for (int i = 0; i < ns; i++) grow(s->spheres[i].position, std::fabs((double)s->spheres[i].radius));
+    for (int i = 0; i < nt; i++)
+        for (int k = 0; k < 3; k++) grow(s->triangles[i].vertices[k], 0.0);
+    for (int i = 0; i < nq; i++)
+        for (int k = 0; k < 4; k++) grow(s->quads[i].vertices[k], 0.0);
+    scale *= 2.0;
+    if (!std::isfinite(scale) || scale > 1e30 || std::getenv("BWRT_NO_CULL")) scale = INFINITY;
+    c->cull_omax = std::isfinite(scale) ? (float)scale : -1.0f;  // -1: no ray is culled
     for (int i = 0; i < nt; i++, id++)
         compile_polygon(h.data() + off_tri + (size_t)i * RT_TRI_FLOATS, hit + (size_t)id * RT_HIT_FLOATS,
-                        s->triangles[i].vertices, 3, s->triangles[i].mat);
+                        s->triangles[i].vertices, 3, s->triangles[i].mat, scale);
     for (int i = 0; i < nq; i++, id++)
         compile_polygon(h.data() + off_quad + (size_t)i * RT_QUAD_FLOATS, hit + (size_t)id * RT_HIT_FLOATS,
-                        s->quads[i].vertices, 4, s->quads[i].mat);
+                        s->quads[i].vertices, 4, s->quads[i].mat, scale);
     // BVH for large scenes (BWRT_BVH_MIN primitives, default 64)
     size_t off_bvh = 0, off_bvh_prims = 0;
     {
@@ -534,6 +602,7 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.n_pln = c->n_pln;
     K.n_tri = c->n_tri;
     K.n_quad = c->n_quad;
+    K.cull_omax = c->cull_omax;
     int nmax = c->n_sph;  // Main.cu:217
     if (c->n_pln > nmax) nmax = c->n_pln;
     if (c->n_tri > nmax) nmax = c->n_tri;
@@ -554,20 +623,22 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
 
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
     unsigned long long* stamps = nullptr;
-    if (std::getenv("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS): per-phase wave-cycle sums
-        if (hipMalloc(&stamps, 8 * sizeof(unsigned long long)) == hipSuccess)
-            (void)hipMemsetAsync(stamps, 0, 8 * sizeof(unsigned long long), s);
+    const int NST = 24;  // 8 per-phase wave-cycle sums + 16 utilisation counters
+    if (std::getenv("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS)
+        if (hipMalloc(&stamps, NST * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemsetAsync(stamps, 0, NST * sizeof(unsigned long long), s);
         K.stamps = stamps;
     }
     K.tile_w = c->tile_w;
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, s);
     if (stamps) {
-        unsigned long long h[8] = {0};
+        unsigned long long h[NST] = {0};
         (void)hipMemcpyAsync(h, stamps, sizeof h, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
-        std::fprintf(stderr, "stamps %llu %llu %llu %llu %llu %llu %llu %llu\n", h[0], h[1], h[2], h[3], h[4], h[5],
-                     h[6], h[7]);
+        std::fprintf(stderr, "stamps");
+        for (int k = 0; k < NST; k++) std::fprintf(stderr, " %llu", h[k]);
+        std::fprintf(stderr, "\n");
         (void)hipFree(stamps);
     }
     if (e != hipSuccess) return hip_fail(c, e, "rt_render_kernel launch");

@@ -209,9 +209,10 @@ __device__ __forceinline__ float specular_weight(f3 i, f3 o, f3 n, f3 m, float r
 
 // genRandomDirection (Main.cu:193-206): rejection-sampled ball point,
 // normalised, flipped into the hemisphere of `normal` (may be non-unit).
-__device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal) {
+__device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters = nullptr) {
     f3 r;
     do {
+        if (iters) ++*iters;
         float x = rand_range(s, 2.0f) - 1.0f;
         float y = rand_range(s, 2.0f) - 1.0f;
         float z = rand_range(s, 2.0f) - 1.0f;
@@ -245,8 +246,38 @@ __device__ __forceinline__ bool polygon_edges(const __attribute__((address_space
     return inside;
 }
 
+// Conservative cull (approximate arithmetic, FMA allowed): skip the exact
+// test when the ray's line passes the polygon's cull sphere {c, Rc^2} with
+//   |w|^2 a (1 - 2^-14) - (w.d)^2 > Rc^2 a,   w = c - o,  a = |d|^2
+// i.e. distance^2 > Rc^2 + 2^-14 |w|^2 (the 2^-14 term dominates the
+// evaluation error, ~2^-22 |w|^2), and only for origins within the scene
+// scale (rt_context.cpp cull_sphere: the reference rejects every such
+// polygon).  NaN/inf rays compare false and are never culled.
+struct CullRay {
+    float a, a_k;  // |d|^2, |d|^2 (1 - 2^-14)
+    bool ok;       // max|o_i| <= K.cull_omax
+};
+
+__device__ __forceinline__ CullRay cull_ray(const rt_kparams& K, f3 o, float a) {
+    CullRay c;
+    c.a = a;
+    c.a_k = a * (1.0f - 6.103515625e-05f);
+    c.ok = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= K.cull_omax;
+    return c;
+}
+
+__device__ __forceinline__ bool culled(const __attribute__((address_space(4))) float* cs, const CullRay& cr, f3 o,
+                                       f3 d) {
+    const float wx = cs[0] - o.x, wy = cs[1] - o.y, wz = cs[2] - o.z;
+    const float ww = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
+    const float pj = __builtin_fmaf(wx, d.x, __builtin_fmaf(wy, d.y, wz * d.z));
+    const float lhs = __builtin_fmaf(-pj, pj, ww * cr.a_k);
+    return cr.ok && lhs > cs[3] * cr.a;
+}
+
 __device__ __forceinline__ void polygon_test(const __attribute__((address_space(4))) float* q, int nv, f3 o, f3 d, int id,
-                                             float& best_t, int& best_id) {
+                                             const CullRay& cr, float& best_t, int& best_id) {
+    if (culled(q + (nv == 3 ? RT_TRI_CULL : RT_QUAD_CULL), cr, o, d)) return;
     float nx = q[0], ny = q[1], nz = q[2], dd = q[3];
     float nd = nx * d.x + ny * d.y + nz * d.z;
     if (!(fabsf(nd) < RT_NEAR_ZERO)) {
@@ -281,6 +312,7 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
     const int pln_base = K.n_sph;
     const int tri_base = K.n_sph + K.n_pln;
     const int quad_base = tri_base + K.n_tri;
+    const CullRay cr = cull_ray(K, o, a);
 #ifdef RT_UNROLL_MAXN
 #pragma unroll
     for (int i = 0; i < RT_UNROLL_MAXN; i++) {
@@ -316,8 +348,9 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
                 }
             }
         }
-        if (i < K.n_tri) polygon_test(as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, best_t, best_id);
-        if (i < K.n_quad) polygon_test(as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, best_t, best_id);
+        if (i < K.n_tri) polygon_test(as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, cr, best_t, best_id);
+        if (i < K.n_quad)
+            polygon_test(as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, cr, best_t, best_id);
     }
 }
 
@@ -678,6 +711,19 @@ rt_render_kernel(rt_kparams K) {
         st_prev = _t;                                         \
     } while (0)
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+    // utilisation counters (wave-level, lane 0 adds): [0] rounds, [1] front
+    // waves, [2] front tasks, [3] rejection-loop wave trips, [4] rejection
+    // lane trips, [5] spec waves, [6] spec tasks, [7] I-phase waves,
+    // [8] I-phase rays
+    unsigned long long st_u[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    auto wave_max = [](int v) {
+        for (int m = 1; m < 64; m <<= 1) v = max(v, __shfl_xor(v, m));
+        return v;
+    };
+    auto wave_sum = [](int v) {
+        for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
+        return v;
+    };
 #else
 #define STAMP(k) \
     do {         \
@@ -946,6 +992,19 @@ rt_render_sorted_kernel(rt_kparams K) {
         st_prev = _t;                                         \
     } while (0)
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+    // utilisation counters (wave-level, lane 0 adds): [0] rounds, [1] front
+    // waves, [2] front tasks, [3] rejection-loop wave trips, [4] rejection
+    // lane trips, [5] spec waves, [6] spec tasks, [7] I-phase waves,
+    // [8] I-phase rays
+    unsigned long long st_u[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    auto wave_max = [](int v) {
+        for (int m = 1; m < 64; m <<= 1) v = max(v, __shfl_xor(v, m));
+        return v;
+    };
+    auto wave_sum = [](int v) {
+        for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
+        return v;
+    };
 #else
 #define STAMP(k) \
     do {         \
@@ -997,6 +1056,9 @@ rt_render_sorted_kernel(rt_kparams K) {
             const int nf = cnt[0], nb = cnt[1];
             const bool do_front = tid < nf;
             const bool do_spec = tid >= BLOCK - nb;
+#ifdef RT_STAMPS
+            int rej_it = 0;
+#endif
             if (do_front || do_spec) {
                 Xorwow rs;
                 rs.d = __float_as_uint(SLOT(7, tid));
@@ -1008,8 +1070,13 @@ rt_render_sorted_kernel(rt_kparams K) {
                 const f3 nrm = mk(SLOT(0, tid), SLOT(1, tid), SLOT(2, tid));
                 const int code = __float_as_int(SLOT(6, tid));
                 f3 r;
+#ifdef RT_STAMPS
+                int* rej_ptr = &rej_it;
+#else
+                int* rej_ptr = nullptr;
+#endif
                 if (do_front) {
-                    r = random_direction(rs, nrm);
+                    r = random_direction(rs, nrm, rej_ptr);
                     if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
                 } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
@@ -1028,6 +1095,22 @@ rt_render_sorted_kernel(rt_kparams K) {
                 SLOT(11, tid) = __uint_as_float(rs.v3);
                 SLOT(12, tid) = __uint_as_float(rs.v4);
             }
+#ifdef RT_STAMPS
+            {
+                const int itl = (do_front && !do_spec) ? rej_it : 0;
+                const unsigned long long bf = __ballot(do_front), bs = __ballot(do_spec);
+                const int mx = wave_max(itl), sm = wave_sum(itl);
+                if (lane == 0) {
+                    st_u[0] += 1;
+                    st_u[1] += bf != 0;
+                    st_u[2] += __popcll(bf);
+                    st_u[3] += mx;
+                    st_u[4] += sm;
+                    st_u[5] += bs != 0;
+                    st_u[6] += __popcll(bs);
+                }
+            }
+#endif
         }
         STAMP(3);
         __syncthreads();
@@ -1068,6 +1151,15 @@ rt_render_sorted_kernel(rt_kparams K) {
         }
 
         STAMP(5);
+#ifdef RT_STAMPS
+        {
+            const unsigned long long br = __ballot(has_ray);
+            if (lane == 0) {
+                st_u[7] += br != 0;
+                st_u[8] += __popcll(br);
+            }
+        }
+#endif
         // ---- I-phase: closest hit + brdfChoice (Main.cu:214-245)
         if (has_ray) {
             has_ray = false;
@@ -1089,8 +1181,10 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(6);
     }
 #ifdef RT_STAMPS
-    if ((threadIdx.x & 63) == 0 && K.stamps)
+    if ((threadIdx.x & 63) == 0 && K.stamps) {
         for (int k = 0; k < 8; k++) atomicAdd(&K.stamps[k], st_acc[k]);
+        for (int k = 0; k < 9; k++) atomicAdd(&K.stamps[8 + k], st_u[k]);
+    }
 #endif
 #undef STAMP
 #undef SLOT

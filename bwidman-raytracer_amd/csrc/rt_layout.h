@@ -12,8 +12,9 @@
 // HBM layout (all float32, records padded to 16 B):
 //   spheres   : n_sph  x  4 floats  {cx, cy, cz, r*r}
 //   planes    : n_pln  x  4 floats  {nx, ny, nz, d}
-//   triangles : n_tri  x 24 floats  {nx,ny,nz,d, v0[3],in0[3], v1[3],in1[3], v2[3],in2[3], pad2}
-//   quads     : n_quad x 28 floats  {nx,ny,nz,d, v0[3],in0[3], .. v3[3],in3[3]}
+//   triangles : n_tri  x 28 floats  {nx,ny,nz,d, v0[3],in0[3], v1[3],in1[3], v2[3],in2[3], pad2,
+//                                    cull sphere {cx,cy,cz,Rc^2}}
+//   quads     : n_quad x 32 floats  {nx,ny,nz,d, v0[3],in0[3], .. v3[3],in3[3], cull {.., Rc^2 = inf}}
 //   hit table : n_prim x 12 floats  {n_or_centre[3], is_sphere,
 //                                    albedo[3], emittance,
 //                                    roughness, ior^2-1, 0, 0}
@@ -29,8 +30,10 @@
 
 #define RT_SPH_FLOATS 4
 #define RT_PLN_FLOATS 4
-#define RT_TRI_FLOATS 24
-#define RT_QUAD_FLOATS 28
+#define RT_TRI_FLOATS 28
+#define RT_QUAD_FLOATS 32
+#define RT_TRI_CULL 24   // offset of the cull sphere in a triangle record
+#define RT_QUAD_CULL 28
 #define RT_HIT_FLOATS 12
 
 #define RT_NEAR_ZERO 0.0001f       // Intersection.cuh:4
@@ -66,6 +69,9 @@ struct rt_kparams {
     // (count << 24) | first index into bvh_prims (global primitive ids).
     const float* bvh_nodes;
     const int* bvh_prims;
+    // conservative polygon culling (see polygon_test): only rays whose origin
+    // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
+    float cull_omax;
 };
 
 // Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,

@@ -87,6 +87,18 @@ def test_stress_c5_rows_bvh(gpu, oracle):
     same_state(gpu, st)
 
 
+def test_stress_brute_force_with_culling(gpu, oracle, monkeypatch):
+    """The stress scene through the brute-force loop (BVH disabled): 10,000
+    random triangles, many of them skinny, exercise the conservative
+    cull-sphere test in front of every exact triangle test."""
+    monkeypatch.setenv("BWRT_BVH_MIN", "100000000")
+    img, st = run_pair(gpu, oracle, scenes.stress_scene(), 96, 54, 2, 8)
+    monkeypatch.delenv("BWRT_BVH_MIN")
+    gpu.set_scene(scenes.scene_07())
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
 @pytest.mark.parametrize("name,w,h,spp,mb", [("07", 320, 180, 4, 5), ("04", 320, 180, 4, 3),
                                               ("04_box", 320, 180, 4, 5), ("01", 256, 256, 1, 1)])
 def test_bvh_forced_on_small_scenes(gpu, oracle, monkeypatch, name, w, h, spp, mb):
