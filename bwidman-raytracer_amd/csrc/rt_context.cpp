@@ -623,7 +623,7 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
 
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
     unsigned long long* stamps = nullptr;
-    const int NST = 24;  // 8 per-phase wave-cycle sums + 16 utilisation counters
+    const int NST = 32;  // 8 per-phase wave-cycle sums + utilisation / branch counters
     if (std::getenv("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS)
         if (hipMalloc(&stamps, NST * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemsetAsync(stamps, 0, NST * sizeof(unsigned long long), s);

@@ -253,6 +253,23 @@ __device__ __forceinline__ bool polygon_edges(const __attribute__((address_space
 // evaluation error, ~2^-22 |w|^2), and only for origins within the scene
 // scale (rt_context.cpp cull_sphere: the reference rejects every such
 // polygon).  NaN/inf rays compare false and are never culled.
+#ifdef RT_STAMPS
+// diagnostic: per-branch wave entries and active lanes -> K.stamps[17 + 2k], [18 + 2k]
+#define RT_BRANCH_COUNT(K, k)                                                                          \
+    do {                                                                                               \
+        const unsigned long long _m = __ballot(1);                                                     \
+        if (__builtin_amdgcn_mbcnt_hi((unsigned)(_m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)_m, 0u)) == 0 && \
+            (K).stamps) {                                                                              \
+            atomicAdd(&(K).stamps[17 + 2 * (k)], 1ull);                                                \
+            atomicAdd(&(K).stamps[18 + 2 * (k)], (unsigned long long)__popcll(_m));                    \
+        }                                                                                              \
+    } while (0)
+#else
+#define RT_BRANCH_COUNT(K, k) \
+    do {                      \
+    } while (0)
+#endif
+
 struct CullRay {
     float a, a_k;  // |d|^2, |d|^2 (1 - 2^-14)
     bool ok;       // max|o_i| <= K.cull_omax
@@ -275,9 +292,10 @@ __device__ __forceinline__ bool culled(const __attribute__((address_space(4))) f
     return cr.ok && lhs > cs[3] * cr.a;
 }
 
-__device__ __forceinline__ void polygon_test(const __attribute__((address_space(4))) float* q, int nv, f3 o, f3 d, int id,
-                                             const CullRay& cr, float& best_t, int& best_id) {
+__device__ __forceinline__ void polygon_test(const rt_kparams& K, const __attribute__((address_space(4))) float* q, int nv,
+                                             f3 o, f3 d, int id, const CullRay& cr, float& best_t, int& best_id) {
     if (culled(q + (nv == 3 ? RT_TRI_CULL : RT_QUAD_CULL), cr, o, d)) return;
+    RT_BRANCH_COUNT(K, 2);
     float nx = q[0], ny = q[1], nz = q[2], dd = q[3];
     float nd = nx * d.x + ny * d.y + nz * d.z;
     if (!(fabsf(nd) < RT_NEAR_ZERO)) {
@@ -286,6 +304,7 @@ __device__ __forceinline__ void polygon_test(const __attribute__((address_space(
         // polygon's own distance test (Intersection.cuh:118-122)
         bool plane_hit = !(t <= RT_NEAR_ZERO || t > INFINITY);
         if (plane_hit && !(t <= RT_NEAR_ZERO || t > best_t)) {
+            RT_BRANCH_COUNT(K, 3);
             f3 P = add(o, scale(t, d));
             if (polygon_edges(q + 4, nv, P)) {
                 best_t = t;
@@ -313,6 +332,7 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
     const int tri_base = K.n_sph + K.n_pln;
     const int quad_base = tri_base + K.n_tri;
     const CullRay cr = cull_ray(K, o, a);
+    RT_BRANCH_COUNT(K, 4);
 #ifdef RT_UNROLL_MAXN
 #pragma unroll
     for (int i = 0; i < RT_UNROLL_MAXN; i++) {
@@ -329,6 +349,7 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
             // exact early-out: b >= 0 (finite disc, a2 > 0) gives -b - sqrt(disc) <= 0,
             // i.e. t <= 0 <= nearZero, rejected by the reference as well
             if (!(disc < 0.0f) && !(b >= 0.0f && disc == disc && a2 > 0.0f)) {
+                RT_BRANCH_COUNT(K, 0);
                 float t = (-b - sqrtf(disc)) / a2;
                 if (!(t <= RT_NEAR_ZERO || t > best_t)) {
                     best_t = t;
@@ -348,9 +369,9 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
                 }
             }
         }
-        if (i < K.n_tri) polygon_test(as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, cr, best_t, best_id);
+        if (i < K.n_tri) polygon_test(K, as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, cr, best_t, best_id);
         if (i < K.n_quad)
-            polygon_test(as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, cr, best_t, best_id);
+            polygon_test(K, as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, cr, best_t, best_id);
     }
 }
 
