@@ -997,12 +997,16 @@ rt_render_sorted_kernel(rt_kparams K) {
         px.az = px.az + lz;
         px.frame++;
         px.passes_left--;
-        if (px.passes_left == 0) {
+        // a finished pixel is stored here only if the lane has another one to
+        // render (persistent grids); otherwise after the loop, by the whole
+        // wave at once
+        if (px.passes_left == 0 && px.w + T < nitems) {
             store_pixel(K, npix, px);
             load_item(K, npix, nitems, px.w + T, px);
         }
         mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
     };
+    bool ended = false;  // path ended this round: finish_path() once, after the I-phase
 
 #ifdef RT_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1165,7 +1169,7 @@ rt_render_sorted_kernel(rt_kparams K) {
                 o = hP;
                 d = r;
                 if (depth > K.max_bounces)  // Main.cu:210
-                    finish_path();
+                    ended = true;
                 else
                     has_ray = true;
             }
@@ -1196,11 +1200,16 @@ rt_render_sorted_kernel(rt_kparams K) {
                 hspec = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE;
                 mode = M_SHADE;
             } else {
-                finish_path();
+                ended = true;
             }
+        }
+        if (ended) {
+            ended = false;
+            finish_path();
         }
         STAMP(6);
     }
+    if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
 #ifdef RT_STAMPS
     if ((threadIdx.x & 63) == 0 && K.stamps) {
         for (int k = 0; k < 8; k++) atomicAdd(&K.stamps[k], st_acc[k]);
