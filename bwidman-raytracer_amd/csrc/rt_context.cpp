@@ -79,6 +79,7 @@ struct rt_context {
     rt_camera camera{};
     int n_sph = 0, n_pln = 0, n_tri = 0, n_quad = 0;
     float cull_omax = 0.0f;  // polygon culling bound (rt_layout.h)
+    int bvh_nodes_per_order = 0;
     DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table | bvh nodes | bvh prims
     size_t off_bvh = 0, off_bvh_prims = 0;  // in floats; 0 = no BVH
     size_t off_pln = 0, off_tri = 0, off_quad = 0, off_hit = 0;  // in floats
@@ -229,26 +230,51 @@ void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_
 }
 
 // ---- BVH over spheres / triangles / quads (large scenes) -------------------
-// Depth-first node array with miss links (rt_layout.h); median split on the
-// widest centroid axis, <= 4 primitives per leaf.  Boxes are inflated by
-// 1e-3 + 1e-4 * |coordinate| — orders of magnitude beyond the rounding of
-// the reference's hit tests — so every hit the reference can accept lies
-// inside its leaf's box.
+// Binned-SAH binary tree, emitted as SIX threaded (stackless) node arrays,
+// one per dominant ray direction (+x, -x, +y, -y, +z, -z): in array k the
+// children of every node are laid out near-first for that direction, each
+// node holding its "miss" link (next node once the subtree is skipped).  A
+// lane walks the array of its ray's dominant axis/sign, so boxes come
+// roughly front to back and the running closest hit prunes the rest
+// (multiple-threaded BVH).  Boxes are inflated by 1e-3 + 1e-4 * |coordinate|
+// — orders of magnitude beyond the rounding of the reference's hit tests —
+// so every hit the reference can accept lies inside its leaf's box.
 struct BvhItem {
     float lo[3], hi[3], c[3];
     int id;
 };
 
+struct BvhNode {
+    float lo[3], hi[3];
+    int left = -1, right = -1;  // children (internal)
+    int first = 0, count = 0;   // prims range (leaf)
+};
+
 struct BvhBuilder {
+    static constexpr int kBins = 16;
+    static constexpr int kMaxLeaf = 8;
     std::vector<BvhItem> items;
-    std::vector<float> nodes;  // 8 floats per node
+    std::vector<BvhNode> tree;
     std::vector<int> prims;
+    std::vector<float> nodes;  // 6 orders x n_nodes x 8 floats
+    int n_nodes = 0;
 
     static float inflate(float v) { return 1e-3f + 1e-4f * std::fabs(v); }
+    static float area(const float* lo, const float* hi) {
+        const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return (dx < 0 || dy < 0 || dz < 0) ? 0.0f : 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+
+    int make_leaf(int node, int b, int e) {
+        tree[node].first = (int)prims.size();
+        tree[node].count = e - b;
+        for (int i = b; i < e; i++) prims.push_back(items[i].id);
+        return node;
+    }
 
     int build(int b, int e) {
-        const int node = (int)(nodes.size() / 8);
-        nodes.resize(nodes.size() + 8);
+        const int node = (int)tree.size();
+        tree.emplace_back();
         float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int i = b; i < e; i++)
@@ -258,42 +284,127 @@ struct BvhBuilder {
                 clo[a] = std::min(clo[a], items[i].c[a]);
                 chi[a] = std::max(chi[a], items[i].c[a]);
             }
-        int leaf = -1;
-        if (e - b <= 4) {
-            leaf = ((e - b) << 24) | (int)prims.size();
-            for (int i = b; i < e; i++) prims.push_back(items[i].id);
-        } else {
-            int axis = 0;
-            for (int a = 1; a < 3; a++)
-                if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
-            const int mid = (b + e) / 2;
-            std::nth_element(items.begin() + b, items.begin() + mid, items.begin() + e,
-                             [axis](const BvhItem& x, const BvhItem& y) {
-                                 return x.c[axis] < y.c[axis] || (x.c[axis] == y.c[axis] && x.id < y.id);
-                             });
-            build(b, mid);
-            build(mid, e);
-        }
-        float* n = &nodes[8 * (size_t)node];
         for (int a = 0; a < 3; a++) {
-            n[a] = lo[a];
-            n[4 + a] = hi[a];
+            tree[node].lo[a] = lo[a];
+            tree[node].hi[a] = hi[a];
         }
-        const int end = (int)(nodes.size() / 8);  // first node after this subtree
-        int miss = -2;                             // patched below
-        std::memcpy(&n[3], &miss, 4);
-        std::memcpy(&n[7], &leaf, 4);
-        subtree_end.resize(end);
-        subtree_end[node] = end;
+        const int n = e - b;
+        if (n <= 2) return make_leaf(node, b, e);
+        // binned SAH over the three axes
+        float best_cost = INFINITY;
+        int best_axis = -1, best_bin = -1;
+        for (int a = 0; a < 3; a++) {
+            const float ext = chi[a] - clo[a];
+            if (!(ext > 0.0f)) continue;
+            int cnt[kBins] = {0};
+            float blo[kBins][3], bhi[kBins][3];
+            for (int k = 0; k < kBins; k++)
+                for (int q = 0; q < 3; q++) {
+                    blo[k][q] = INFINITY;
+                    bhi[k][q] = -INFINITY;
+                }
+            for (int i = b; i < e; i++) {
+                int k = (int)((items[i].c[a] - clo[a]) / ext * kBins);
+                k = std::min(std::max(k, 0), kBins - 1);
+                cnt[k]++;
+                for (int q = 0; q < 3; q++) {
+                    blo[k][q] = std::min(blo[k][q], items[i].lo[q]);
+                    bhi[k][q] = std::max(bhi[k][q], items[i].hi[q]);
+                }
+            }
+            float rarea[kBins];
+            int rcnt[kBins];
+            float rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int rc = 0;
+            for (int k = kBins - 1; k > 0; k--) {
+                rc += cnt[k];
+                for (int q = 0; q < 3; q++) {
+                    rl[q] = std::min(rl[q], blo[k][q]);
+                    rh[q] = std::max(rh[q], bhi[k][q]);
+                }
+                rarea[k] = area(rl, rh);
+                rcnt[k] = rc;
+            }
+            float ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int lc = 0;
+            for (int k = 0; k < kBins - 1; k++) {
+                lc += cnt[k];
+                for (int q = 0; q < 3; q++) {
+                    ll[q] = std::min(ll[q], blo[k][q]);
+                    lh[q] = std::max(lh[q], bhi[k][q]);
+                }
+                if (lc == 0 || rcnt[k + 1] == 0) continue;
+                const float cost = area(ll, lh) * lc + rarea[k + 1] * rcnt[k + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = a;
+                    best_bin = k;
+                }
+            }
+        }
+        const float leaf_cost = area(lo, hi) * n;
+        int mid;
+        if (best_axis >= 0 && (best_cost < leaf_cost || n > kMaxLeaf)) {
+            const int a = best_axis;
+            const float ext = chi[a] - clo[a];
+            auto it = std::partition(items.begin() + b, items.begin() + e, [&](const BvhItem& x) {
+                int k = (int)((x.c[a] - clo[a]) / ext * kBins);
+                k = std::min(std::max(k, 0), kBins - 1);
+                return k <= best_bin;
+            });
+            mid = (int)(it - items.begin());
+        } else if (n <= kMaxLeaf) {
+            return make_leaf(node, b, e);
+        } else {  // all centroids equal: split in the middle
+            mid = (b + e) / 2;
+        }
+        if (mid <= b || mid >= e) mid = (b + e) / 2;
+        const int l = build(b, mid);
+        const int r = build(mid, e);
+        tree[node].left = l;
+        tree[node].right = r;
         return node;
     }
-    std::vector<int> subtree_end;
+
+    // threaded array for direction `order` (axis = order / 2, negative = order & 1)
+    void emit(int order, int node, std::vector<int>& pos, std::vector<int>& seq) {
+        pos[node] = (int)seq.size();
+        seq.push_back(node);
+        const BvhNode& t = tree[node];
+        if (t.left < 0) return;
+        const int a = order / 2;
+        const float cl = tree[t.left].lo[a] + tree[t.left].hi[a];
+        const float cr = tree[t.right].lo[a] + tree[t.right].hi[a];
+        const bool left_first = (order & 1) ? !(cl < cr) : (cl <= cr);
+        emit(order, left_first ? t.left : t.right, pos, seq);
+        emit(order, left_first ? t.right : t.left, pos, seq);
+    }
 
     void finish() {
-        const int total = (int)(nodes.size() / 8);
-        for (int i = 0; i < total; i++) {
-            const int miss = subtree_end[i] < total ? subtree_end[i] : -1;
-            std::memcpy(&nodes[8 * (size_t)i + 3], &miss, 4);
+        n_nodes = (int)tree.size();
+        nodes.assign((size_t)6 * n_nodes * 8, 0.0f);
+        std::vector<int> pos(n_nodes), seq, end(n_nodes);
+        for (int order = 0; order < 6; order++) {
+            seq.clear();
+            emit(order, 0, pos, seq);
+            // subtree end in this order: position after the last descendant
+            for (int i = n_nodes - 1; i >= 0; i--) {
+                const BvhNode& t = tree[seq[i]];
+                end[i] = t.left < 0 ? i + 1 : std::max(end[pos[t.left]], end[pos[t.right]]);
+            }
+            float* base = nodes.data() + (size_t)order * n_nodes * 8;
+            for (int i = 0; i < n_nodes; i++) {
+                const BvhNode& t = tree[seq[i]];
+                float* nd = base + (size_t)i * 8;
+                for (int a = 0; a < 3; a++) {
+                    nd[a] = t.lo[a];
+                    nd[4 + a] = t.hi[a];
+                }
+                const int miss = end[i] < n_nodes ? end[i] : -1;
+                const int leaf = t.left < 0 ? ((t.count << 24) | t.first) : -1;
+                std::memcpy(&nd[3], &miss, 4);
+                std::memcpy(&nd[7], &leaf, 4);
+            }
         }
     }
 
@@ -469,8 +580,10 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             };
             for (int i = 0; i < nt; i++) poly(ns + np + i, s->triangles[i].vertices, 3);
             for (int i = 0; i < nq; i++) poly(ns + np + nt + i, s->quads[i].vertices, 4);
+            B.tree.reserve(2 * (size_t)nb);
             B.build(0, nb);
             B.finish();
+            c->bvh_nodes_per_order = B.n_nodes;
             off_bvh = (total + 3) & ~(size_t)3;
             off_bvh_prims = off_bvh + B.nodes.size();
             h.resize(off_bvh_prims + B.prims.size() + 4, 0.0f);
@@ -603,6 +716,7 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.n_tri = c->n_tri;
     K.n_quad = c->n_quad;
     K.cull_omax = c->cull_omax;
+    K.bvh_order_stride = c->bvh_nodes_per_order * 8;
     int nmax = c->n_sph;  // Main.cu:217
     if (c->n_pln > nmax) nmax = c->n_pln;
     if (c->n_tri > nmax) nmax = c->n_tri;

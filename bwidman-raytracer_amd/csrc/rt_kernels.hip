@@ -73,7 +73,7 @@ __device__ __forceinline__ unsigned next_u32(Xorwow& s) {
     s.v1 = s.v2;
     s.v2 = s.v3;
     s.v3 = s.v4;
-    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.v4 = s.v4 ^ (s.v4 << 4) ^ (t ^ (t << 1));  // v_xor3_b32
     s.d += 362437u;
     return s.v4 + s.d;
 }
@@ -209,13 +209,20 @@ __device__ __forceinline__ float specular_weight(f3 i, f3 o, f3 n, f3 m, float r
 
 // genRandomDirection (Main.cu:193-206): rejection-sampled ball point,
 // normalised, flipped into the hemisphere of `normal` (may be non-unit).
+// randRange(2) - 1 in one rounding: float(u) * 2^-31 is exact (power-of-two
+// scaling of a float, no under/overflow), so fma(float(u), 2^-31, -1) =
+// RN(RN(float(u) * 2^-31) - 1), bit-identical to the two-step reference.
+__device__ __forceinline__ float rand_pm1(Xorwow& s) {
+    return __builtin_fmaf((float)next_u32(s), 4.656612873077393e-10f, -1.0f);
+}
+
 __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters = nullptr) {
     f3 r;
     do {
         if (iters) ++*iters;
-        float x = rand_range(s, 2.0f) - 1.0f;
-        float y = rand_range(s, 2.0f) - 1.0f;
-        float z = rand_range(s, 2.0f) - 1.0f;
+        float x = rand_pm1(s);
+        float y = rand_pm1(s);
+        float z = rand_pm1(s);
         r = mk(x, y, z);
         // length(r) > 1 (Main.cu:197) <=> RN(x*x+y*y+z*z) > 1 + 2^-23: sqrt is
         // correctly rounded, so RN(sqrt(s)) > 1 iff s >= 1 + 2^-22 (checked
@@ -473,10 +480,14 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
     const f3 dc = mk(fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x, fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y,
                      fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z);
     const f3 inv = mk(1.0f / dc.x, 1.0f / dc.y, 1.0f / dc.z);
+    // node array of the ray's dominant direction (near children first)
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const int order = (ax >= ay && ax >= az) ? (d.x < 0.0f) : (ay >= az ? 2 + (d.y < 0.0f) : 4 + (d.z < 0.0f));
+    const float* nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
     int node = 0;
     while (node >= 0) {
-        const float4 lo = *reinterpret_cast<const float4*>(K.bvh_nodes + 8 * node);
-        const float4 hi = *reinterpret_cast<const float4*>(K.bvh_nodes + 8 * node + 4);
+        const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
+        const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
         const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
         const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
         const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;

@@ -63,12 +63,15 @@ struct rt_kparams {
     unsigned long long* stamps; // diagnostic builds (-DRT_STAMPS) only: per-phase cycle sums
     int tile_w;                 // wave tile width in pixels (1..64, power of 2); 0 = linear order
     // bounding-volume hierarchy over spheres/triangles/quads (large scenes;
-    // null = brute-force loop).  nodes: 8 floats {bmin.xyz, miss, bmax.xyz,
-    // leaf}, depth-first order (first child = node + 1), miss = next node
-    // when the subtree is skipped (-1 = done), leaf = -1 (internal) or
+    // null = brute-force loop): 6 threaded node arrays (one per dominant ray
+    // direction +x,-x,+y,-y,+z,-z; bvh_order_stride floats apart).  Node: 8
+    // floats {bmin.xyz, miss, bmax.xyz, leaf}, depth-first (first child =
+    // node + 1, near child first for that direction), miss = next node when
+    // the subtree is skipped (-1 = done), leaf = -1 (internal) or
     // (count << 24) | first index into bvh_prims (global primitive ids).
     const float* bvh_nodes;
     const int* bvh_prims;
+    int bvh_order_stride;
     // conservative polygon culling (see polygon_test): only rays whose origin
     // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
     float cull_omax;
