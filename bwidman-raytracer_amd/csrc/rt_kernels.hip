@@ -484,28 +484,50 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
     const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
     const int order = (ax >= ay && ax >= az) ? (d.x < 0.0f) : (ay >= az ? 2 + (d.y < 0.0f) : 4 + (d.z < 0.0f));
     const float* nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
+    // speculative while-while traversal (Aila & Laine): a lane that reaches a
+    // leaf its ray enters parks it and walks on; the parked leaves are tested
+    // together once every lane has one parked (or ran out of nodes, or
+    // reached a second leaf, where it waits), so the primitive tests run on
+    // full waves and no lane idles in the node loop while others search.
     int node = 0;
-    while (node >= 0) {
-        const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
-        const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
-        const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
-        const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
-        const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
-        const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-        const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-        // margins: 1e-5 relative + 1e-6 absolute on the interval, and prune
-        // against the current closest distance only beyond the same margin
-        const bool hit = tmin <= tmax * (1.0f + 1e-5f) + 1e-6f && tmin <= best_t * (1.0f + 1e-5f) + 1e-5f;
-        const int miss = __float_as_int(lo.w);
-        const int leaf = __float_as_int(hi.w);
-        if (!hit) {
-            node = miss;
-        } else if (leaf < 0) {
-            node = node + 1;
-        } else {
+    while (true) {
+        int leaf = -1;
+        while (true) {
+            bool stalled = false;
+            if (node >= 0) {
+                RT_BRANCH_COUNT(K, 5);
+                const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
+                const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
+                const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
+                const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
+                const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+                const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+                // margins: 1e-5 relative + 1e-6 absolute on the interval, and prune
+                // against the current closest distance only beyond the same margin
+                const bool hit = tmin <= tmax * (1.0f + 1e-5f) + 1e-6f && tmin <= best_t * (1.0f + 1e-5f) + 1e-5f;
+                const int miss = __float_as_int(lo.w);
+                const int lf = __float_as_int(hi.w);
+                if (!hit) {
+                    node = miss;
+                } else if (lf < 0) {
+                    node = node + 1;
+                } else if (leaf < 0) {
+                    leaf = lf;  // park it, walk on
+                    node = miss;
+                } else {
+                    stalled = true;  // second leaf: revisit after the parked one
+                }
+            }
+            if (__all(leaf >= 0 || node < 0 || stalled)) break;
+        }
+        if (!__any(leaf >= 0)) break;
+        if (leaf >= 0) {
             const int first = leaf & 0xffffff, count = leaf >> 24;
-            for (int k = 0; k < count; k++) prim_test(K, K.bvh_prims[first + k], o, d, a2, a4, best_t, best_id, best_key);
-            node = miss;
+            for (int k = 0; k < count; k++) {
+                RT_BRANCH_COUNT(K, 6);
+                prim_test(K, K.bvh_prims[first + k], o, d, a2, a4, best_t, best_id, best_key);
+            }
         }
     }
 }
