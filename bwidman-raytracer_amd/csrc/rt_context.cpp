@@ -230,12 +230,12 @@ void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_
 }
 
 // ---- BVH over spheres / triangles / quads (large scenes) -------------------
-// Binned-SAH binary tree, emitted as SIX threaded (stackless) node arrays,
-// one per dominant ray direction (+x, -x, +y, -y, +z, -z): in array k the
-// children of every node are laid out near-first for that direction, each
+// Binned-SAH binary tree, emitted as EIGHT threaded (stackless) node arrays,
+// one per ray-direction octant: in array k the children of every node are
+// laid out near side of the node's split axis first for that octant, each
 // node holding its "miss" link (next node once the subtree is skipped).  A
-// lane walks the array of its ray's dominant axis/sign, so boxes come
-// roughly front to back and the running closest hit prunes the rest
+// lane walks the array of its ray's octant, so boxes come front to back
+// along every split and the running closest hit prunes the rest
 // (multiple-threaded BVH).  Boxes are inflated by 1e-3 + 1e-4 * |coordinate|
 // — orders of magnitude beyond the rounding of the reference's hit tests —
 // so every hit the reference can accept lies inside its leaf's box.
@@ -247,12 +247,14 @@ struct BvhItem {
 struct BvhNode {
     float lo[3], hi[3];
     int left = -1, right = -1;  // children (internal)
+    int axis = 0;               // split axis (internal): left child holds the smaller centroids
     int first = 0, count = 0;   // prims range (leaf)
 };
 
 struct BvhBuilder {
     static constexpr int kBins = 16;
-    static constexpr int kMaxLeaf = 8;
+    int max_leaf = 8;         // BWRT_BVH_LEAF
+    float trav_cost = 0.0f;   // BWRT_BVH_CT: SAH cost of one node step relative to one primitive test
     std::vector<BvhItem> items;
     std::vector<BvhNode> tree;
     std::vector<int> prims;
@@ -343,8 +345,9 @@ struct BvhBuilder {
             }
         }
         const float leaf_cost = area(lo, hi) * n;
+        best_cost += trav_cost * area(lo, hi);
         int mid;
-        if (best_axis >= 0 && (best_cost < leaf_cost || n > kMaxLeaf)) {
+        if (best_axis >= 0 && (best_cost < leaf_cost || n > max_leaf)) {
             const int a = best_axis;
             const float ext = chi[a] - clo[a];
             auto it = std::partition(items.begin() + b, items.begin() + e, [&](const BvhItem& x) {
@@ -353,7 +356,7 @@ struct BvhBuilder {
                 return k <= best_bin;
             });
             mid = (int)(it - items.begin());
-        } else if (n <= kMaxLeaf) {
+        } else if (n <= max_leaf) {
             return make_leaf(node, b, e);
         } else {  // all centroids equal: split in the middle
             mid = (b + e) / 2;
@@ -361,30 +364,29 @@ struct BvhBuilder {
         if (mid <= b || mid >= e) mid = (b + e) / 2;
         const int l = build(b, mid);
         const int r = build(mid, e);
+        tree[node].axis = best_axis >= 0 ? best_axis : 0;
         tree[node].left = l;
         tree[node].right = r;
         return node;
     }
 
-    // threaded array for direction `order` (axis = order / 2, negative = order & 1)
+    // threaded array for the ray-direction octant `order` (bit a set: d[a] < 0):
+    // at every node the child on the near side of its split axis comes first
     void emit(int order, int node, std::vector<int>& pos, std::vector<int>& seq) {
         pos[node] = (int)seq.size();
         seq.push_back(node);
         const BvhNode& t = tree[node];
         if (t.left < 0) return;
-        const int a = order / 2;
-        const float cl = tree[t.left].lo[a] + tree[t.left].hi[a];
-        const float cr = tree[t.right].lo[a] + tree[t.right].hi[a];
-        const bool left_first = (order & 1) ? !(cl < cr) : (cl <= cr);
+        const bool left_first = !((order >> t.axis) & 1);
         emit(order, left_first ? t.left : t.right, pos, seq);
         emit(order, left_first ? t.right : t.left, pos, seq);
     }
 
     void finish() {
         n_nodes = (int)tree.size();
-        nodes.assign((size_t)6 * n_nodes * 8, 0.0f);
+        nodes.assign((size_t)8 * n_nodes * 8, 0.0f);
         std::vector<int> pos(n_nodes), seq, end(n_nodes);
-        for (int order = 0; order < 6; order++) {
+        for (int order = 0; order < 8; order++) {
             seq.clear();
             emit(order, 0, pos, seq);
             // subtree end in this order: position after the last descendant
@@ -581,6 +583,8 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             for (int i = 0; i < nt; i++) poly(ns + np + i, s->triangles[i].vertices, 3);
             for (int i = 0; i < nq; i++) poly(ns + np + nt + i, s->quads[i].vertices, 4);
             B.tree.reserve(2 * (size_t)nb);
+            if (const char* e = std::getenv("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 255);
+            if (const char* e = std::getenv("BWRT_BVH_CT")) B.trav_cost = (float)std::atof(e);
             B.build(0, nb);
             B.finish();
             c->bvh_nodes_per_order = B.n_nodes;

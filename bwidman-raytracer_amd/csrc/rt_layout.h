@@ -63,10 +63,10 @@ struct rt_kparams {
     unsigned long long* stamps; // diagnostic builds (-DRT_STAMPS) only: per-phase cycle sums
     int tile_w;                 // wave tile width in pixels (1..64, power of 2); 0 = linear order
     // bounding-volume hierarchy over spheres/triangles/quads (large scenes;
-    // null = brute-force loop): 6 threaded node arrays (one per dominant ray
-    // direction +x,-x,+y,-y,+z,-z; bvh_order_stride floats apart).  Node: 8
+    // null = brute-force loop): 8 threaded node arrays (one per ray-direction
+    // octant, bit a = d[a] < 0; bvh_order_stride floats apart).  Node: 8
     // floats {bmin.xyz, miss, bmax.xyz, leaf}, depth-first (first child =
-    // node + 1, near child first for that direction), miss = next node when
+    // node + 1, near side of the split first for that octant), miss = next node when
     // the subtree is skipped (-1 = done), leaf = -1 (internal) or
     // (count << 24) | first index into bvh_prims (global primitive ids).
     const float* bvh_nodes;
