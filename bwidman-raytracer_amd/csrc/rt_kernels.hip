@@ -213,11 +213,20 @@ __device__ __forceinline__ float specular_weight(f3 i, f3 o, f3 n, f3 m, float r
 // scaling of a float, no under/overflow), so fma(float(u), 2^-31, -1) =
 // RN(RN(float(u) * 2^-31) - 1), bit-identical to the two-step reference.
 __device__ __forceinline__ float rand_pm1(Xorwow& s) {
+#ifdef RT_REJ_NOFMA
+    return rand_range(s, 2.0f) - 1.0f;
+#else
     return __builtin_fmaf((float)next_u32(s), 4.656612873077393e-10f, -1.0f);
+#endif
 }
 
 __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters = nullptr) {
     f3 r;
+    // 5 trips = 15 XORWOW steps bring the 5-word state back to its registers:
+    // unrolling by 5 removes the per-trip register rotation
+#ifdef RT_REJ_UNROLL
+#pragma unroll RT_REJ_UNROLL
+#endif
     do {
         if (iters) ++*iters;
         float x = rand_pm1(s);
