@@ -1079,7 +1079,6 @@ rt_render_sorted_kernel(rt_kparams K) {
     while (true) {
         const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
         STAMP(7);
-        if (!__syncthreads_or(task != T_NONE)) break;
         STAMP(0);
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
@@ -1116,10 +1115,13 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(1);
         __syncthreads();
         STAMP(2);
+        // no task anywhere in the workgroup: every lane is idle (rays are
+        // always consumed in the round that made them), so the group is done
+        const int nf = cnt[0], nb = cnt[1];
+        if (nf + nb == 0) break;
 
         // ---- T-phase: execute slot `tid`
         {
-            const int nf = cnt[0], nb = cnt[1];
             const bool do_front = tid < nf;
             const bool do_spec = tid >= BLOCK - nb;
 #ifdef RT_STAMPS
