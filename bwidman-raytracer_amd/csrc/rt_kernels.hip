@@ -1334,6 +1334,18 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
 #endif
     if (small_block) return launch_block<64, true>(K, hit_lds, lds, grid_mult, num_cus, stream);
     const size_t lds_s = rt_render_lds_bytes(K, RT_SORTED_BLOCK, hit_lds, true);
+    // deep paths (large max_bounces) make the LDS record stack big: take
+    // 128-lane groups when they keep more waves resident per CU (LDS 160 KB,
+    // VGPR-bound at 4 x RT_WAVES_PER_EU waves)
+    auto waves_per_cu = [](size_t lds_bytes, int block) {
+        const long by_lds = (long)(160 * 1024 / (lds_bytes ? lds_bytes : 1)) * (block / 64);
+        return by_lds < 4L * RT_WAVES_PER_EU ? by_lds : 4L * RT_WAVES_PER_EU;
+    };
+    if (RT_SORTED_BLOCK > 128 &&
+        waves_per_cu(rt_render_lds_bytes(K, 128, hit_lds, true), 128) > waves_per_cu(lds_s, RT_SORTED_BLOCK)) {
+        const size_t lds_128 = rt_render_lds_bytes(K, 128, hit_lds, true);
+        return launch_block<128, true>(K, hit_lds, lds_128, grid_mult, num_cus, stream);
+    }
     return launch_block<RT_SORTED_BLOCK, true>(K, hit_lds, lds_s, grid_mult, num_cus, stream);
 }
 
