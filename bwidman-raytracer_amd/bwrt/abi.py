@@ -77,6 +77,8 @@ class RenderParams(C.Structure):
 
 
 RT_OK = 0
+RT_ERR_INVALID_ARGUMENT = -1
+RT_ERR_NO_DEVICE = -2
 RT_MAX_BOUNCES = 32
 RT_DEFAULT_MAX_BOUNCES = 5
 
@@ -97,6 +99,10 @@ def _proto(lib):
         "rt_reset_accumulation": (C.c_int, [vp]),
         "rt_frame_counter": (C.c_uint, [vp]),
         "rt_set_max_bounces": (C.c_int, [vp, C.c_int]),
+        "rt_set_background": (C.c_int, [vp, C.c_float, C.c_float, C.c_float]),
+        "rt_get_camera": (C.c_int, [vp, P(Camera)]),
+        "rt_apply_controls": (C.c_int, [P(Camera), C.c_uint, C.c_float]),
+        "rt_controls": (C.c_int, [vp, C.c_uint, C.c_float]),
         "rt_init_rand": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int]),
         "rt_render": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp]),
         "rt_render_ex": (C.c_int, [vp, P(RenderParams), vp, vp]),
@@ -139,6 +145,13 @@ def load(path: str | None = None):
     if path is None:
         _lib = lib
     return lib
+
+
+# Controls.cuh key bits (include/rt_abi.h RT_KEY_*)
+KEYS = {"W": 1 << 0, "A": 1 << 1, "S": 1 << 2, "D": 1 << 3, "SPACE": 1 << 4, "LEFT_SHIFT": 1 << 5,
+        "LEFT": 1 << 6, "RIGHT": 1 << 7, "UP": 1 << 8, "DOWN": 1 << 9, "ESCAPE": 1 << 10}
+CONTROLS_MOVED = 1
+CONTROLS_QUIT = 2
 
 
 class RTError(RuntimeError):

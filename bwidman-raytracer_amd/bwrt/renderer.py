@@ -62,6 +62,28 @@ class Renderer:
     def set_max_bounces(self, mb: int):
         self._check(self.lib.rt_set_max_bounces(self.ctx, mb))
 
+    def set_background(self, r: float, g: float, b: float):
+        """backgroundColor (Main.cu:27): radiance of misses and the depth cut-off."""
+        self._check(self.lib.rt_set_background(self.ctx, r, g, b))
+
+    def get_camera(self):
+        from .abi import Camera
+        cam = Camera()
+        self._check(self.lib.rt_get_camera(self.ctx, C.byref(cam)))
+        return cam
+
+    def controls(self, keys, delta_time: float) -> int:
+        """controls() (Controls.cuh:5-75) for one frame: `keys` is an int mask
+        or an iterable of key names ("W", "LEFT", ...).  Returns the
+        RT_CONTROLS_* flags; movement restarts accumulation."""
+        from .abi import KEYS
+        if not isinstance(keys, int):
+            keys = sum(KEYS[k] for k in keys)
+        flags = self.lib.rt_controls(self.ctx, keys, delta_time)
+        if flags < 0:
+            self._check(flags)
+        return flags
+
     def init_rand(self, width, height, row_offset=0, row_stride=1):
         self._check(self.lib.rt_init_rand(self.ctx, width, height, row_offset, row_stride))
 

@@ -79,6 +79,7 @@ struct rt_context {
     rt_camera camera{};
     int n_sph = 0, n_pln = 0, n_tri = 0, n_quad = 0;
     float cull_omax = 0.0f;  // polygon culling bound (rt_layout.h)
+    float background[3] = {0.0f, 0.0f, 0.0f};  // backgroundColor, Main.cu:27
     int bvh_nodes_per_order = 0;
     DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table | bvh nodes | bvh prims
     size_t off_bvh = 0, off_bvh_prims = 0;  // in floats; 0 = no BVH
@@ -623,6 +624,93 @@ int rt_set_camera(rt_context* c, const rt_camera* cam) {
     return RT_OK;
 }
 
+int rt_set_background(rt_context* c, float r, float g, float b) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    c->background[0] = r;
+    c->background[1] = g;
+    c->background[2] = b;
+    return RT_OK;
+}
+
+int rt_get_camera(const rt_context* c, rt_camera* cam) {
+    if (!c || !cam) return RT_ERR_INVALID_ARGUMENT;
+    *cam = c->camera;
+    return RT_OK;
+}
+
+// Controls.cuh:5-75 in the reference's float operation order: the direction
+// vectors are rotY * rotX (matrix product, Math.cuh:191-199) times a basis
+// vector (mat * vec = row dots, Math.cuh:144-150); position +/-= k * dir.
+int rt_apply_controls(rt_camera* cam, unsigned keys, float dt) {
+    if (!cam) return RT_ERR_INVALID_ARGUMENT;
+    const float move = 5 * dt;
+    const float rot = 2 * dt;
+    const float cy = cosf(cam->angle[0]), sy = sinf(cam->angle[0]);  // rotationMatrix3DY
+    const float cx = cosf(cam->angle[1]), sx = sinf(cam->angle[1]);  // rotationMatrix3DX
+    const float L[3][3] = {{cy, 0, sy}, {0, 1, 0}, {-sy, 0, cy}};
+    const float U[3][3] = {{1, 0, 0}, {0, cx, -sx}, {0, sx, cx}};
+    float M[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) M[i][j] = L[i][0] * U[0][j] + L[i][1] * U[1][j] + L[i][2] * U[2][j];
+    auto mul = [&](float x, float y, float z) {
+        return V3{M[0][0] * x + M[0][1] * y + M[0][2] * z, M[1][0] * x + M[1][1] * y + M[1][2] * z,
+                  M[2][0] * x + M[2][1] * y + M[2][2] * z};
+    };
+    const V3 front = mul(0, 0, -1), right = mul(1, 0, 0);
+    rt_vec3& p = cam->position;
+    int flags = 0;
+    auto add = [&](float k, V3 v, float sign) {  // position (+|-)= k * v
+        const V3 kv{k * v.x, k * v.y, k * v.z};
+        if (sign > 0) {
+            p.x = p.x + kv.x;
+            p.y = p.y + kv.y;
+            p.z = p.z + kv.z;
+        } else {
+            p.x = p.x - kv.x;
+            p.y = p.y - kv.y;
+            p.z = p.z - kv.z;
+        }
+        flags |= RT_CONTROLS_MOVED;
+    };
+    if (keys & RT_KEY_W) add(move, front, +1);
+    if (keys & RT_KEY_A) add(move, right, -1);
+    if (keys & RT_KEY_S) add(move, front, -1);
+    if (keys & RT_KEY_D) add(move, right, +1);
+    if (keys & RT_KEY_SPACE) {
+        p.y += move;
+        flags |= RT_CONTROLS_MOVED;
+    }
+    if (keys & RT_KEY_LEFT_SHIFT) {
+        p.y -= move;
+        flags |= RT_CONTROLS_MOVED;
+    }
+    if (keys & RT_KEY_LEFT) {
+        cam->angle[0] += rot;
+        flags |= RT_CONTROLS_MOVED;
+    }
+    if (keys & RT_KEY_RIGHT) {
+        cam->angle[0] -= rot;
+        flags |= RT_CONTROLS_MOVED;
+    }
+    if (keys & RT_KEY_UP) {
+        cam->angle[1] += rot;
+        flags |= RT_CONTROLS_MOVED;
+    }
+    if (keys & RT_KEY_DOWN) {
+        cam->angle[1] -= rot;
+        flags |= RT_CONTROLS_MOVED;
+    }
+    if (keys & RT_KEY_ESCAPE) flags |= RT_CONTROLS_QUIT;
+    return flags;
+}
+
+int rt_controls(rt_context* c, unsigned keys, float dt) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    const int flags = rt_apply_controls(&c->camera, keys, dt);
+    if (flags > 0 && (flags & RT_CONTROLS_MOVED)) c->frame = 1;  // accumulatedFrames = 1
+    return flags;
+}
+
 int rt_reset_accumulation(rt_context* c) {
     if (!c) return RT_ERR_INVALID_ARGUMENT;
     c->frame = 1;
@@ -715,6 +803,9 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
                 K.rot[3 * i + j] = L[i][0] * U[0][j] + L[i][1] * U[1][j] + L[i][2] * U[2][j];
     }
     K.jitter = (float)(0.001 * (p->width / 1000));  // Main.cu:291
+    K.bg[0] = c->background[0];
+    K.bg[1] = c->background[1];
+    K.bg[2] = c->background[2];
     K.n_sph = c->n_sph;
     K.n_pln = c->n_pln;
     K.n_tri = c->n_tri;

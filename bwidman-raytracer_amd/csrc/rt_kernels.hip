@@ -269,7 +269,7 @@ __device__ __forceinline__ bool polygon_edges(const __attribute__((address_space
 // evaluation error, ~2^-22 |w|^2), and only for origins within the scene
 // scale (rt_context.cpp cull_sphere: the reference rejects every such
 // polygon).  NaN/inf rays compare false and are never culled.
-#ifdef RT_STAMPS
+#if defined(RT_STAMPS) && defined(RT_BRANCH_STATS)
 // diagnostic: per-branch wave entries and active lanes -> K.stamps[17 + 2k], [18 + 2k]
 #define RT_BRANCH_COUNT(K, k)                                                                          \
     do {                                                                                               \
@@ -695,11 +695,11 @@ __device__ __forceinline__ f3 specular_scatter(Xorwow& rs, f3 d, f3 n, float rou
 //   brdf = kspec * {1,1,1} (specular) or 4 * albedo (diffuse, :259).
 template <int BLOCK>
 __device__ __forceinline__ void fold_records(const int* rec_code, const float* rec_k, const float* rec_c,
-                                             int depth, const float* hit_tab, float& lx, float& ly,
-                                             float& lz) {
-    lx = 0.0f;
-    ly = 0.0f;
-    lz = 0.0f;  // backgroundColor
+                                             int depth, const float* hit_tab, const float* bg, float& lx,
+                                             float& ly, float& lz) {
+    lx = bg[0];  // backgroundColor (Main.cu:209-211): the miss / depth cut-off radiance
+    ly = bg[1];
+    lz = bg[2];
     for (int l = depth - 1; l >= 0; --l) {
         const int c0 = rec_code[l * BLOCK];
         const float k = rec_k[l * BLOCK];
@@ -882,7 +882,7 @@ rt_render_kernel(rt_kparams K) {
             if (finished) {
                 // (4) fold the recursion innermost-first (Main.cu:262-268):
                 //     L = emitted + (brdf * L) * cosAngle
-                float lx = 0.0f, ly = 0.0f, lz = 0.0f;  // backgroundColor
+                float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor
                 for (int l = depth - 1; l >= 0; --l) {
                     const int c0 = rec_code[l * BLOCK];
                     const float k = rec_k[l * BLOCK];
@@ -1027,7 +1027,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     // path end: fold, accumulate (Main.cu:299-304), next frame / next pixel
     auto finish_path = [&]() {
         float lx, ly, lz;
-        fold_records<BLOCK>(rec_code, rec_k, rec_c, depth, hit_tab, lx, ly, lz);
+        fold_records<BLOCK>(rec_code, rec_k, rec_c, depth, hit_tab, K.bg, lx, ly, lz);
         if (px.frame == 1u) {
             px.ax = 0.0f;
             px.ay = 0.0f;

@@ -51,6 +51,7 @@ struct rt_kparams {
     float rot[9];               // rotationMatrix3DY(a0) * rotationMatrix3DX(a1), row-major
     float screen_z;             // Main.cu:336
     float jitter;               // (float)(0.001 * (width / 1000)), Main.cu:291
+    float bg[3];                // backgroundColor, Main.cu:27
     int n_sph, n_pln, n_tri, n_quad, n_max;
     const float* sph;
     const float* pln;

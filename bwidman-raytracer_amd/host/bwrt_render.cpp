@@ -1,12 +1,21 @@
-// bwrt_render — C++ host driver over the C ABI (the reference's main loop,
-// /root/reference/bwidman-raytracer/src/Main.cu:401-517, without the GLFW
-// window: frames are rendered progressively, FPS / sample count are printed
-// once per second like Main.cu:486-495, and the final image is written as a
-// binary PPM (top row first, i.e. the RGBA8 buffer flipped: row 0 = bottom).
+// bwrt_render — C++ host driver over the C ABI: the reference's main loop
+// (/root/reference/bwidman-raytracer/src/Main.cu:401-517) without the GLFW
+// window.  Frames are rendered progressively; after each frame controls()
+// (Controls.cuh:5-75) is applied with the keys a scripted timeline holds
+// (--keys) and the frame's duration (or a fixed --dt); FPS / sample count
+// are printed once per second like Main.cu:486-495; the final image is
+// written as PNG or PPM (top row first: the buffer's row 0 is the bottom).
 //
-//   bwrt_render [--scene 07|01|04|04_box] [--width 1920] [--height 1080]
-//               [--frames 8] [--frames-per-call 1] [--max-bounces 5]
-//               [--device 0] [--out image.ppm] [--dump-scene file.bin]
+//   bwrt_render [--scene 07|01|04|04_box | --scene-file FILE] [--save-scene FILE]
+//               [--width 1920] [--height 1080] [--frames 8] [--frames-per-call 1]
+//               [--max-bounces 5] [--background r,g,b] [--device 0]
+//               [--keys "W*10,W+LEFT*5,*3"] [--dt SECONDS]
+//               [--out image.png|image.ppm] [--dump-scene file.bin]
+//
+// --keys: comma-separated steps KEY[+KEY...]*FRAMES (keys W A S D SPACE
+// LEFT_SHIFT LEFT RIGHT UP DOWN ESCAPE; an empty key list holds nothing);
+// the timeline repeats its last step.  ESCAPE ends the loop like
+// glfwSetWindowShouldClose.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -14,7 +23,9 @@
 #include <string>
 #include <vector>
 
+#include "image_io.hpp"
 #include "rt_abi.h"
+#include "scene_file.hpp"
 #include "scenes.hpp"
 
 static int die(rt_context* ctx, int rc, const char* what) {
@@ -22,18 +33,79 @@ static int die(rt_context* ctx, int rc, const char* what) {
     return 1;
 }
 
+struct KeyStep {
+    unsigned keys;
+    int frames;
+};
+
+static bool parse_keys(const std::string& spec, std::vector<KeyStep>& steps) {
+    static const struct {
+        const char* name;
+        unsigned bit;
+    } names[] = {{"W", RT_KEY_W},         {"A", RT_KEY_A},       {"S", RT_KEY_S},
+                 {"D", RT_KEY_D},         {"SPACE", RT_KEY_SPACE}, {"LEFT_SHIFT", RT_KEY_LEFT_SHIFT},
+                 {"LEFT", RT_KEY_LEFT},   {"RIGHT", RT_KEY_RIGHT}, {"UP", RT_KEY_UP},
+                 {"DOWN", RT_KEY_DOWN},   {"ESCAPE", RT_KEY_ESCAPE}};
+    size_t pos = 0;
+    while (pos <= spec.size()) {
+        size_t end = spec.find(',', pos);
+        if (end == std::string::npos) end = spec.size();
+        std::string step = spec.substr(pos, end - pos);
+        pos = end + 1;
+        if (step.empty()) {
+            if (end == spec.size()) break;
+            continue;
+        }
+        int frames = 1;
+        const size_t star = step.find('*');
+        if (star != std::string::npos) {
+            frames = std::atoi(step.c_str() + star + 1);
+            step = step.substr(0, star);
+            if (frames < 1) return false;
+        }
+        unsigned keys = 0;
+        size_t k = 0;
+        while (k < step.size()) {
+            size_t plus = step.find('+', k);
+            if (plus == std::string::npos) plus = step.size();
+            const std::string name = step.substr(k, plus - k);
+            bool found = false;
+            for (const auto& n : names)
+                if (name == n.name) {
+                    keys |= n.bit;
+                    found = true;
+                }
+            if (!found) return false;
+            k = plus + 1;
+        }
+        steps.push_back({keys, frames});
+    }
+    return true;
+}
+
 int main(int argc, char** argv) {
-    std::string scene_name = "07", out, dump;
+    std::string scene_name = "07", scene_file, save, out, dump, keys_spec;
     int width = 1920, height = 1080, frames = 8, per_call = 1, max_bounces = RT_DEFAULT_MAX_BOUNCES, device = 0;
+    float bg[3] = {0.0f, 0.0f, 0.0f};
+    double fixed_dt = -1.0;
     for (int i = 1; i < argc; i++) {
         auto next = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : ""; };
         if (!std::strcmp(argv[i], "--scene")) scene_name = next();
+        else if (!std::strcmp(argv[i], "--scene-file")) scene_file = next();
+        else if (!std::strcmp(argv[i], "--save-scene")) save = next();
         else if (!std::strcmp(argv[i], "--width")) width = std::atoi(next());
         else if (!std::strcmp(argv[i], "--height")) height = std::atoi(next());
         else if (!std::strcmp(argv[i], "--frames")) frames = std::atoi(next());
         else if (!std::strcmp(argv[i], "--frames-per-call")) per_call = std::atoi(next());
         else if (!std::strcmp(argv[i], "--max-bounces")) max_bounces = std::atoi(next());
-        else if (!std::strcmp(argv[i], "--device")) device = std::atoi(next());
+        else if (!std::strcmp(argv[i], "--background")) {
+            if (std::sscanf(next(), "%f,%f,%f", &bg[0], &bg[1], &bg[2]) != 3) {
+                std::fprintf(stderr, "--background expects r,g,b\n");
+                return 2;
+            }
+        } else if (!std::strcmp(argv[i], "--device")) device = std::atoi(next());
+        else if (!std::strcmp(argv[i], "--keys")) keys_spec = next();
+        else if (!std::strcmp(argv[i], "--dt")) fixed_dt = std::atof(next());
         else if (!std::strcmp(argv[i], "--out")) out = next();
         else if (!std::strcmp(argv[i], "--dump-scene")) dump = next();
         else {
@@ -41,10 +113,31 @@ int main(int argc, char** argv) {
             return 2;
         }
     }
-    bwrt::SceneData sd = scene_name == "01" ? bwrt::scene01()
-                         : scene_name == "04" ? bwrt::scene04()
-                         : scene_name == "04_box" ? bwrt::scene04box()
-                                                  : bwrt::scene07();
+    std::vector<KeyStep> steps;
+    if (!keys_spec.empty()) {
+        if (!parse_keys(keys_spec, steps)) {
+            std::fprintf(stderr, "bad --keys '%s'\n", keys_spec.c_str());
+            return 2;
+        }
+        per_call = 1;  // controls() runs between frames
+    }
+    bwrt::SceneData sd;
+    if (!scene_file.empty()) {
+        const std::string err = bwrt::load_scene(scene_file, sd);
+        if (!err.empty()) {
+            std::fprintf(stderr, "%s: %s\n", scene_file.c_str(), err.c_str());
+            return 2;
+        }
+    } else {
+        sd = scene_name == "01"       ? bwrt::scene01()
+             : scene_name == "04"     ? bwrt::scene04()
+             : scene_name == "04_box" ? bwrt::scene04box()
+                                      : bwrt::scene07();
+    }
+    if (!save.empty() && !bwrt::save_scene(save, sd)) {
+        std::fprintf(stderr, "cannot write %s\n", save.c_str());
+        return 1;
+    }
     if (!dump.empty()) {  // camera + primitive bytes (compared with bwrt.scenes by the tests)
         FILE* f = std::fopen(dump.c_str(), "wb");
         if (!f) return 1;
@@ -54,40 +147,59 @@ int main(int argc, char** argv) {
         std::fwrite(sd.triangles.data(), sizeof(rt_triangle), sd.triangles.size(), f);
         std::fwrite(sd.quads.data(), sizeof(rt_quad), sd.quads.size(), f);
         std::fclose(f);
-        return 0;
     }
+    if (!dump.empty() || (!save.empty() && frames <= 0)) return 0;
+
     rt_context* ctx = nullptr;
     int rc = rt_create(device, &ctx);
     if (rc) return die(ctx, rc, "rt_create");
     rt_scene view = sd.view();
     if ((rc = rt_set_scene(ctx, &view))) return die(ctx, rc, "rt_set_scene");
     if ((rc = rt_set_max_bounces(ctx, max_bounces))) return die(ctx, rc, "rt_set_max_bounces");
+    if ((rc = rt_set_background(ctx, bg[0], bg[1], bg[2]))) return die(ctx, rc, "rt_set_background");
     std::vector<uint8_t> rgba((size_t)width * height * 4);
     using clk = std::chrono::steady_clock;
     double delta = 0.0;
     int frame_count = 0;
-    for (int done = 0; done < frames;) {
+    size_t step = 0;
+    int step_left = steps.empty() ? 0 : steps[0].frames;
+    for (int done = 0; done < frames;) {  // Main.cu:471-496
         const int n = std::min(per_call, frames - done);
         auto t0 = clk::now();
         if ((rc = rt_render(ctx, width, height, n, rgba.data()))) return die(ctx, rc, "rt_render");
         done += n;
-        delta += std::chrono::duration<double>(clk::now() - t0).count();
+        const double frame_s = std::chrono::duration<double>(clk::now() - t0).count();
+        bool quit = false;
+        if (!steps.empty()) {  // controls(window, camera, deltaTime, accumulatedFrames)
+            const unsigned keys = steps[step].keys;
+            if (--step_left == 0 && step + 1 < steps.size()) step_left = steps[++step].frames;
+            const int flags = rt_controls(ctx, keys, (float)(fixed_dt >= 0 ? fixed_dt : frame_s));
+            if (flags < 0) return die(ctx, flags, "rt_controls");
+            quit = flags & RT_CONTROLS_QUIT;
+        }
+        delta += frame_s;
         frame_count += n;
-        if (delta > 1.0 || done == frames) {  // Main.cu:486-495
+        if (delta > 1.0 || done == frames || quit) {  // Main.cu:486-495
             std::printf("FPS: %d | Samples: %u | kernel %.3f ms\n", (int)(frame_count / delta),
                         rt_frame_counter(ctx) - 1, rt_last_kernel_ms(ctx));
             delta = 0.0;
             frame_count = 0;
         }
+        if (quit) break;
     }
     if (!out.empty()) {
-        FILE* f = std::fopen(out.c_str(), "wb");
-        if (!f) return 1;
-        std::fprintf(f, "P6\n%d %d\n255\n", width, height);
-        for (int y = height - 1; y >= 0; y--)
-            for (int x = 0; x < width; x++) std::fwrite(&rgba[((size_t)y * width + x) * 4], 1, 3, f);
-        std::fclose(f);
+        const bool png = out.size() > 4 && out.compare(out.size() - 4, 4, ".png") == 0;
+        const bool ok = png ? bwrt::write_png(out, width, height, rgba.data())
+                            : bwrt::write_ppm(out, width, height, rgba.data());
+        if (!ok) {
+            std::fprintf(stderr, "cannot write %s\n", out.c_str());
+            return 1;
+        }
     }
+    rt_camera cam;
+    if (!steps.empty() && rt_get_camera(ctx, &cam) == RT_OK)
+        std::printf("camera %.9g %.9g %.9g %.9g %.9g\n", cam.position.x, cam.position.y, cam.position.z,
+                    cam.angle[0], cam.angle[1]);
     rt_destroy(ctx);
     return 0;
 }

@@ -180,6 +180,43 @@ RT_API unsigned rt_frame_counter(const rt_context* ctx);
 /* Default max_bounces for rt_render() (initially RT_DEFAULT_MAX_BOUNCES). */
 RT_API int rt_set_max_bounces(rt_context* ctx, int max_bounces);
 
+/* backgroundColor (Main.cu:27, a compile-time constant {0,0,0} there): the
+ * radiance of a miss and of the depth cut-off (Main.cu:209-211).  Takes
+ * effect at the next render; does not reset accumulation. */
+RT_API int rt_set_background(rt_context* ctx, float r, float g, float b);
+
+/* Copy of the context's current camera (after rt_controls()). */
+RT_API int rt_get_camera(const rt_context* ctx, rt_camera* camera);
+
+/* ---- camera controls (Controls.cuh:5-75) ----------------------------------
+ * `keys` = OR of the RT_KEY_* held during the frame, `delta_time` = that
+ * frame's duration in seconds (Main.cu:482).  Movement speed 5/s, rotation
+ * speed 2 rad/s, directions from rotY(angle[0]) * rotX(angle[1]) applied to
+ * (0,0,-1) / (1,0,0), evaluated in float in the reference's operation order.
+ * Returns an OR of RT_CONTROLS_MOVED (any movement key: accumulation restarts,
+ * accumulatedFrames = 1) and RT_CONTROLS_QUIT (escape), or a negative
+ * rt_status. */
+#define RT_KEY_W          (1u << 0)  /* forward */
+#define RT_KEY_A          (1u << 1)  /* left */
+#define RT_KEY_S          (1u << 2)  /* back */
+#define RT_KEY_D          (1u << 3)  /* right */
+#define RT_KEY_SPACE      (1u << 4)  /* up (world y) */
+#define RT_KEY_LEFT_SHIFT (1u << 5)  /* down (world y) */
+#define RT_KEY_LEFT       (1u << 6)  /* yaw +   (angle[0]) */
+#define RT_KEY_RIGHT      (1u << 7)  /* yaw -   */
+#define RT_KEY_UP         (1u << 8)  /* pitch + (angle[1]) */
+#define RT_KEY_DOWN       (1u << 9)  /* pitch - */
+#define RT_KEY_ESCAPE     (1u << 10) /* glfwSetWindowShouldClose */
+#define RT_CONTROLS_MOVED 1
+#define RT_CONTROLS_QUIT 2
+
+/* Apply one frame of controls to a camera (no context, no GPU). */
+RT_API int rt_apply_controls(rt_camera* camera, unsigned keys, float delta_time);
+
+/* Apply one frame of controls to the context's camera; on movement the
+ * frame counter restarts at 1 (the next render resets frameSum). */
+RT_API int rt_controls(rt_context* ctx, unsigned keys, float delta_time);
+
 /* Allocate and seed the per-pixel state for a (width,height) image shard:
  * curand_init(y*width+x, 0, 0) per pixel (Main.cu:369-380) and a frameSum
  * buffer (Main.cu:464-465).  Called implicitly by the render entry points

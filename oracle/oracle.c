@@ -360,10 +360,13 @@ static vec3 random_direction(uint32_t st[6], vec3 normal) {           /* :193-20
 
 /* ---------------------------------------------------------------------- */
 static unsigned long long g_queries, g_paths;
+static vec3 g_background = {0.0f, 0.0f, 0.0f};                        /* Main.cu:27 */
+
+void orc_set_background(float r, float g, float b) { g_background = v3(r, g, b); }
 
 static vec3 trace_path(ray3 in, const orc_scene* sc, uint32_t st[6], int bounces,
                        int max_bounces, unsigned long long* queries) { /* Main.cu:208-272 */
-    vec3 out = v3(0, 0, 0);                                          /* backgroundColor */
+    vec3 out = g_background;                                          /* backgroundColor */
     if (bounces > max_bounces) return out;
     (*queries)++;
     hit_info closest = hit_init();

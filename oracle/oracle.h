@@ -67,6 +67,10 @@ int orc_render_rows(const orc_scene* scene, int width, int height,
                     uint32_t* rng, float* accum, uint8_t* rgba,
                     int init_rng, int threads);
 
+/* backgroundColor (Main.cu:27; {0,0,0} in the reference build) used by the
+ * next orc_render_rows calls. */
+void orc_set_background(float r, float g, float b);
+
 /* Work counters of the last orc_render_rows call (closest-hit queries and
  * paths), for the measured work profile in DESIGN.md. */
 void orc_last_counters(unsigned long long* queries, unsigned long long* paths);

@@ -44,6 +44,8 @@ def lib():
                                       C.c_uint, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_int, C.c_int]
         L.orc_render_rows.restype = C.c_int
+        L.orc_set_background.argtypes = [C.c_float, C.c_float, C.c_float]
+        L.orc_set_background.restype = None
         L.orc_last_counters.argtypes = [C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
         L.orc_last_counters.restype = None
         _lib = L
@@ -77,9 +79,10 @@ class OracleState:
 
 
 def render(scene, state: OracleState, passes: int, max_bounces: int,
-           first_frame: int | None = None, threads: int = 0) -> np.ndarray:
+           first_frame: int | None = None, threads: int = 0, background=(0.0, 0.0, 0.0)) -> np.ndarray:
     """Render `passes` progressive frames; returns the RGBA8 rows (row 0 = bottom)."""
     ff = state.frame if first_frame is None else first_frame
+    lib().orc_set_background(*[float(c) for c in background])
     rc = lib().orc_render_rows(C.cast(scene.ptr(), C.c_void_p), state.width, state.height,
                                state.row_offset, state.row_stride, state.rows, ff, passes,
                                max_bounces, state.rng.ctypes.data, state.accum.ctypes.data,

@@ -218,6 +218,48 @@ def test_camera_moved(gpu, oracle):
     assert np.array_equal(img, st2.rgba)
 
 
+def test_controls_drive_the_camera(gpu, oracle):
+    """rt_controls (Controls.cuh:5-75): a frame with W + LEFT held moves and
+    turns the context camera and restarts accumulation; the next frames
+    match the oracle rendering the moved camera from accumulatedFrames = 1
+    with the RNG streams continuing."""
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    gpu.init_rand(160, 90)
+    gpu.render(160, 90, 2, 4, first_frame=1)
+    assert gpu.frame_counter == 3
+    flags = gpu.controls(["W", "LEFT", "UP"], 0.05)
+    assert flags == 1 and gpu.frame_counter == 1
+    cam = gpu.get_camera()
+    assert cam.angle[0] == np.float32(0.1) and cam.angle[1] == np.float32(0.1)
+    assert gpu.controls([], 0.05) == 0 and gpu.frame_counter == 1
+    img = gpu.render(160, 90, 3, 4)
+    st = oracle.OracleState(160, 90)
+    oracle.render(scenes.scene_07(), st, 2, 4, first_frame=1)
+    s.set_camera(cam)
+    oracle.render(s, st, 3, 4, first_frame=1)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+def test_background_color(gpu, oracle):
+    """backgroundColor (Main.cu:27) as a runtime setting: misses and the
+    depth cut-off return it; bit-exact with the oracle."""
+    s = scenes.scene_07()
+    gpu.set_background(0.25, 0.5, 1.0)
+    try:
+        gpu.set_scene(s)
+        gpu.init_rand(200, 120)
+        img = gpu.render(200, 120, 3, 2, first_frame=1)
+    finally:
+        gpu.set_background(0.0, 0.0, 0.0)
+    st = oracle.OracleState(200, 120)
+    oracle.render(s, st, 3, 2, first_frame=1, background=(0.25, 0.5, 1.0))
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+    assert img[-1, 0, 2] > 100  # the sky (top row) is now blue
+
+
 def test_converges_to_reference_png(gpu):
     """Real-CUDA sanity (statistical): 1024 frames of the 07 scene at
     1920x1080, maxBounces 5 (Main.cu:26) vs Renders/07_specular_BRDF.png:
@@ -286,3 +328,32 @@ def test_render_device_into_torch_buffer(gpu, oracle):
     st = oracle.render_image(s, w, h, 3, 4)
     assert np.array_equal(img, st.rgba)
     assert gpu.last_kernel_ms() > 0
+
+
+def test_cli_progressive_loop_with_controls(bwrt_lib, oracle, tmp_path):
+    """The C++ host loop (host/bwrt_render.cpp, Main.cu:467-496): 2 frames,
+    then W+LEFT held for one frame (controls() restarts accumulation), then 4
+    more frames; the PNG (top row first) equals the oracle's image of the
+    moved camera from accumulatedFrames = 1 with the RNG streams continuing."""
+    import ctypes as C
+    import subprocess
+    from PIL import Image
+    from bwrt.abi import KEYS
+    cli = os.path.join(os.path.dirname(GOLDEN), "..", "bwidman-raytracer_amd", "bin", "bwrt_render")
+    png = tmp_path / "out.png"
+    r = subprocess.run([cli, "--scene", "07", "--width", "160", "--height", "90", "--frames", "6",
+                        "--keys", "*1,W+LEFT*1,*9", "--dt", "0.05", "--out", str(png)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    s = scenes.scene_07()
+    cam = s.camera
+    moved = type(cam).from_buffer_copy(bytes(cam))
+    assert bwrt_lib.rt_apply_controls(C.byref(moved), KEYS["W"] | KEYS["LEFT"], 0.05) == 1
+    st = oracle.OracleState(160, 90)
+    oracle.render(s, st, 2, 5, first_frame=1)
+    s2 = scenes.scene_07()
+    s2.set_camera(moved)
+    oracle.render(s2, st, 4, 5, first_frame=1)
+    img = np.asarray(Image.open(png).convert("RGBA"))[::-1]
+    assert np.array_equal(img, st.rgba)
+    assert "camera" in r.stdout and "Samples: 4" in r.stdout
