@@ -1004,13 +1004,26 @@ rt_render_sorted_kernel(rt_kparams K) {
     float* rec_k = rec_base + levels * BLOCK + tid;
     float* rec_c = rec_base + 2 * levels * BLOCK + tid;
     float* slots = rec_base + 3 * levels * BLOCK;
+#ifdef RT_MAILBOX
+    float* mbox = slots + 13 * BLOCK;  // task results: r.xyz, kspec, rng[6]
+    int* counters = reinterpret_cast<int*>(mbox + 10 * BLOCK);
+#define MBOX(f, i) mbox[(f) * BLOCK + (i)]
+#else
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
+#endif
     // counters[0..3]: queue fronts/backs (2 parities)
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
     if (tid < 4) counters[tid] = 0;
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
+// task results {r.xyz, kspec, rng[6]}: a separate mailbox (RT_MAILBOX), or
+// written back over the slot's own fields {0..3, 7..12}
+#ifdef RT_MAILBOX
+#define RES(f, i) MBOX(f, i)
+#else
+#define RES(f, i) slots[((f) < 4 ? (f) : (f) + 3) * BLOCK + (i)]
+#endif
 
     const long T = (long)gridDim.x * BLOCK;
     PixelState px;
@@ -1079,6 +1092,11 @@ rt_render_sorted_kernel(rt_kparams K) {
     while (true) {
         const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
         STAMP(7);
+#ifndef RT_MAILBOX
+        // every owner has read its previous task result out of the slots
+        // before any wave overwrites them with this round's tasks
+        __syncthreads();
+#endif
         STAMP(0);
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
@@ -1119,6 +1137,15 @@ rt_render_sorted_kernel(rt_kparams K) {
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
         if (nf + nb == 0) break;
+#ifdef RT_MAILBOX
+        // next round's counters were last read before the previous round's
+        // second barrier; the barrier after the execute step orders this
+        // reset before any wave posts next round's tasks
+        if (tid == 0) {
+            counters[2 * (parity ^ 1)] = 0;
+            counters[2 * (parity ^ 1) + 1] = 0;
+        }
+#endif
 
         // ---- T-phase: execute slot `tid`
         {
@@ -1151,17 +1178,17 @@ rt_render_sorted_kernel(rt_kparams K) {
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
                     float kspec;
                     r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
-                    SLOT(3, tid) = kspec;
+                    RES(3, tid) = kspec;
                 }
-                SLOT(0, tid) = r.x;
-                SLOT(1, tid) = r.y;
-                SLOT(2, tid) = r.z;
-                SLOT(7, tid) = __uint_as_float(rs.d);
-                SLOT(8, tid) = __uint_as_float(rs.v0);
-                SLOT(9, tid) = __uint_as_float(rs.v1);
-                SLOT(10, tid) = __uint_as_float(rs.v2);
-                SLOT(11, tid) = __uint_as_float(rs.v3);
-                SLOT(12, tid) = __uint_as_float(rs.v4);
+                RES(0, tid) = r.x;
+                RES(1, tid) = r.y;
+                RES(2, tid) = r.z;
+                RES(4, tid) = __uint_as_float(rs.d);
+                RES(5, tid) = __uint_as_float(rs.v0);
+                RES(6, tid) = __uint_as_float(rs.v1);
+                RES(7, tid) = __uint_as_float(rs.v2);
+                RES(8, tid) = __uint_as_float(rs.v3);
+                RES(9, tid) = __uint_as_float(rs.v4);
             }
 #ifdef RT_STAMPS
             {
@@ -1183,21 +1210,23 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(3);
         __syncthreads();
         STAMP(4);
+#ifndef RT_MAILBOX
         if (tid == 0) {
             counters[2 * (parity ^ 1)] = 0;
             counters[2 * (parity ^ 1) + 1] = 0;
         }
+#endif
         parity ^= 1;
 
         // ---- owner: take the task result back
         if (slot >= 0) {
-            const f3 r = mk(SLOT(0, slot), SLOT(1, slot), SLOT(2, slot));
-            px.rs.d = __float_as_uint(SLOT(7, slot));
-            px.rs.v0 = __float_as_uint(SLOT(8, slot));
-            px.rs.v1 = __float_as_uint(SLOT(9, slot));
-            px.rs.v2 = __float_as_uint(SLOT(10, slot));
-            px.rs.v3 = __float_as_uint(SLOT(11, slot));
-            px.rs.v4 = __float_as_uint(SLOT(12, slot));
+            const f3 r = mk(RES(0, slot), RES(1, slot), RES(2, slot));
+            px.rs.d = __float_as_uint(RES(4, slot));
+            px.rs.v0 = __float_as_uint(RES(5, slot));
+            px.rs.v1 = __float_as_uint(RES(6, slot));
+            px.rs.v2 = __float_as_uint(RES(7, slot));
+            px.rs.v3 = __float_as_uint(RES(8, slot));
+            px.rs.v4 = __float_as_uint(RES(9, slot));
             mode = M_IDLE;
             if (task == T_REGEN) {
                 o = cam;
@@ -1206,7 +1235,7 @@ rt_render_sorted_kernel(rt_kparams K) {
                 has_ray = true;
             } else {
                 rec_code[depth * BLOCK] = task == T_SPEC ? ~hid : hid;
-                rec_k[depth * BLOCK] = task == T_SPEC ? SLOT(3, slot) : 0.0f;
+                rec_k[depth * BLOCK] = task == T_SPEC ? RES(3, slot) : 0.0f;
                 rec_c[depth * BLOCK] = dot(r, hn);  // cosAngle, Main.cu:264
                 depth++;
                 o = hP;
@@ -1261,6 +1290,10 @@ rt_render_sorted_kernel(rt_kparams K) {
 #endif
 #undef STAMP
 #undef SLOT
+#undef RES
+#ifdef RT_MAILBOX
+#undef MBOX
+#endif
 }
 
 // ---- launchers (host side) ------------------------------------------------
@@ -1312,7 +1345,11 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     size_t b = hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
+#ifdef RT_MAILBOX
+    if (sorted) b += (size_t)23 * block * sizeof(float) + 4 * sizeof(int);
+#else
     if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
+#endif
     return b;
 }
 

@@ -357,3 +357,22 @@ def test_cli_progressive_loop_with_controls(bwrt_lib, oracle, tmp_path):
     img = np.asarray(Image.open(png).convert("RGBA"))[::-1]
     assert np.array_equal(img, st.rgba)
     assert "camera" in r.stdout and "Samples: 4" in r.stdout
+
+
+def test_repeated_renders_are_identical(gpu, oracle):
+    """Race check: the workgroup task queue must give the same bits every
+    time, including right after a launch with a different LDS layout (the
+    07 scene at 4 bounces vs the 04 scene at 3)."""
+    cases = [(scenes.scene_04(), 640, 360, 4, 3), (scenes.scene_07(), 640, 360, 4, 4)]
+    want = []
+    for s, w, h, spp, mb in cases:
+        st = oracle.OracleState(w, h)
+        oracle.render(s, st, spp, mb, first_frame=1)
+        want.append(st)
+    for _ in range(6):
+        for (s, w, h, spp, mb), st in zip(cases, want):
+            gpu.set_scene(s)
+            gpu.init_rand(w, h)
+            img = gpu.render(w, h, spp, mb, first_frame=1)
+            assert np.array_equal(img, st.rgba)
+            same_state(gpu, st)
