@@ -693,26 +693,24 @@ __device__ __forceinline__ f3 specular_scatter(Xorwow& rs, f3 d, f3 n, float rou
 // Fold of the recursion innermost-first (Main.cu:262-268):
 //   L = emitted + (brdf * L) * cosAngle,  emitted = emittance * albedo,
 //   brdf = kspec * {1,1,1} (specular) or 4 * albedo (diffuse, :259).
+__device__ __forceinline__ void fold_level(int c0, float k, float c, const float* hit_tab, float& lx, float& ly,
+                                           float& lz) {
+    const bool spec = c0 < 0;
+    const float4 mat = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * (spec ? ~c0 : c0) + 4);
+    const float ex = mat.w * mat.x, ey = mat.w * mat.y, ez = mat.w * mat.z;
+    const float dk = (float)(2.0 / (1 - RT_SPECULAR_CHANCE));  // 4.0f
+    const float bx = spec ? k : dk * mat.x, by = spec ? k : dk * mat.y, bz = spec ? k : dk * mat.z;
+    lx = ex + (bx * lx) * c;
+    ly = ey + (by * ly) * c;
+    lz = ez + (bz * lz) * c;
+}
+
+// Folds levels depth-1 .. 0 of the LDS record stack into L (in/out).
 template <int BLOCK>
 __device__ __forceinline__ void fold_records(const int* rec_code, const float* rec_k, const float* rec_c,
-                                             int depth, const float* hit_tab, const float* bg, float& lx,
-                                             float& ly, float& lz) {
-    lx = bg[0];  // backgroundColor (Main.cu:209-211): the miss / depth cut-off radiance
-    ly = bg[1];
-    lz = bg[2];
-    for (int l = depth - 1; l >= 0; --l) {
-        const int c0 = rec_code[l * BLOCK];
-        const float k = rec_k[l * BLOCK];
-        const float c = rec_c[l * BLOCK];
-        const bool spec = c0 < 0;
-        const float4 mat = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * (spec ? ~c0 : c0) + 4);
-        const float ex = mat.w * mat.x, ey = mat.w * mat.y, ez = mat.w * mat.z;
-        const float dk = (float)(2.0 / (1 - RT_SPECULAR_CHANCE));  // 4.0f
-        const float bx = spec ? k : dk * mat.x, by = spec ? k : dk * mat.y, bz = spec ? k : dk * mat.z;
-        lx = ex + (bx * lx) * c;
-        ly = ey + (by * ly) * c;
-        lz = ez + (bz * lz) * c;
-    }
+                                             int depth, const float* hit_tab, float& lx, float& ly, float& lz) {
+    for (int l = depth - 1; l >= 0; --l)
+        fold_level(rec_code[l * BLOCK], rec_k[l * BLOCK], rec_c[l * BLOCK], hit_tab, lx, ly, lz);
 }
 
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
@@ -999,7 +997,10 @@ rt_render_sorted_kernel(rt_kparams K) {
         hit_tab = smem;
         rec_base = smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3);
     }
-    const int levels = K.max_bounces + 1;
+    // levels 0 .. max_bounces-1 in LDS; the deepest level (max_bounces) ends
+    // the path in the round it is made, so it is folded straight from the
+    // lane's own task slot (fields 4..6, free once the result is taken)
+    const int levels = K.max_bounces;
     int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
     float* rec_k = rec_base + levels * BLOCK + tid;
     float* rec_c = rec_base + 2 * levels * BLOCK + tid;
@@ -1038,9 +1039,12 @@ rt_render_sorted_kernel(rt_kparams K) {
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
 
     // path end: fold, accumulate (Main.cu:299-304), next frame / next pixel
-    auto finish_path = [&]() {
-        float lx, ly, lz;
-        fold_records<BLOCK>(rec_code, rec_k, rec_c, depth, hit_tab, K.bg, lx, ly, lz);
+    auto finish_path = [&](int slot) {
+        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
+        if (depth > K.max_bounces)  // deepest level, parked in the slot
+            fold_level(__float_as_int(SLOT(6, slot)), SLOT(4, slot), SLOT(5, slot), hit_tab, lx, ly, lz);
+        fold_records<BLOCK>(rec_code, rec_k, rec_c, depth > K.max_bounces ? K.max_bounces : depth, hit_tab, lx, ly,
+                            lz);
         if (px.frame == 1u) {
             px.ax = 0.0f;
             px.ay = 0.0f;
@@ -1234,16 +1238,23 @@ rt_render_sorted_kernel(rt_kparams K) {
                 depth = 0;
                 has_ray = true;
             } else {
-                rec_code[depth * BLOCK] = task == T_SPEC ? ~hid : hid;
-                rec_k[depth * BLOCK] = task == T_SPEC ? RES(3, slot) : 0.0f;
-                rec_c[depth * BLOCK] = dot(r, hn);  // cosAngle, Main.cu:264
-                depth++;
-                o = hP;
-                d = r;
-                if (depth > K.max_bounces)  // Main.cu:210
-                    ended = true;
-                else
+                const int code = task == T_SPEC ? ~hid : hid;
+                const float kspec = task == T_SPEC ? RES(3, slot) : 0.0f;
+                const float cosang = dot(r, hn);  // cosAngle, Main.cu:264
+                if (depth < K.max_bounces) {
+                    rec_code[depth * BLOCK] = code;
+                    rec_k[depth * BLOCK] = kspec;
+                    rec_c[depth * BLOCK] = cosang;
+                    o = hP;
+                    d = r;
                     has_ray = true;
+                } else {  // next query would exceed maxBounces (Main.cu:210): the path ends
+                    SLOT(4, slot) = kspec;
+                    SLOT(5, slot) = cosang;
+                    SLOT(6, slot) = __int_as_float(code);
+                    ended = true;
+                }
+                depth++;
             }
         }
 
@@ -1277,7 +1288,7 @@ rt_render_sorted_kernel(rt_kparams K) {
         }
         if (ended) {
             ended = false;
-            finish_path();
+            finish_path(slot);
         }
         STAMP(6);
     }
@@ -1344,7 +1355,8 @@ hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_
 size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
-    size_t b = hit + (size_t)3 * (K.max_bounces + 1) * block * sizeof(float);
+    // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
+    size_t b = hit + (size_t)3 * (K.max_bounces + (sorted ? 0 : 1)) * block * sizeof(float);
 #ifdef RT_MAILBOX
     if (sorted) b += (size_t)23 * block * sizeof(float) + 4 * sizeof(int);
 #else
