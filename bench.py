@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(scenes.CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true",
+                    help="rank 0 re-renders the whole frame on its GPU alone and checks the gathered image")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
     return ap.parse_args()
@@ -99,16 +101,23 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU (LOCAL_RANK); the modulo only matters when ranks
+    # are rehearsed on fewer GPUs than ranks (BWRT_DIST_BACKEND=gloo)
+    dev_index = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    backend = os.environ.get("BWRT_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     lib = abi.load()
     hip_libs = sorted({l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l})
     if len(hip_libs) != 1:
         print(f"warning: {len(hip_libs)} HIP runtimes loaded: {hip_libs}", file=sys.stderr)
-    r = Renderer(local, lib=lib)
+    r = Renderer(dev_index, lib=lib)
     scene = scenes.SCENES[scene_key]()
     r.set_scene(scene)
     plan = ShardPlan(H, world, rank)
@@ -185,7 +194,7 @@ def main():
             "config": {"workload": f"07_specular_BRDF {W}x{H} {SPP}spp {MB}-bounce (BASELINE configs[2])"
                        if args.config == "c3" else f"{args.config}: scene {scene_key} {W}x{H} {SPP}spp {MB}-bounce",
                        "scene": scene_key, "width": W, "height": H, "spp": SPP, "max_bounces": MB,
-                       "parallelism": f"pixel-rows/{world}" + (" + rccl all_gather" if world > 1 else "")},
+                       "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} all_gather" if world > 1 else "")},
             "ms_per_frame": round(ms_step, 4),
             "kernel_ms_avg": round(kern_avg_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -212,6 +221,24 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene_key, W, H, SPP, MB, args.cpu_threads)
         print(json.dumps(out), flush=True)
+    if args.verify:
+        # one more sharded + gathered frame from freshly seeded RNG streams
+        # must equal rank 0 rendering the whole frame alone
+        r.init_rand(W, H, plan.row_offset, plan.row_stride)
+        step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            got = full_img.cpu()
+            solo = torch.empty(H * W, dtype=torch.int32, device=dev)
+            r.init_rand(W, H)
+            r.render_device(r.params(W, H, SPP, MB, first_frame=1), solo.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            same = torch.equal(got, solo.cpu())
+            print(f"verify: {world}-rank gathered frame {'==' if same else '!='} 1-GPU frame", flush=True)
+            if not same:
+                raise SystemExit(1)
     r.close()
     if world > 1:
         dist.destroy_process_group()

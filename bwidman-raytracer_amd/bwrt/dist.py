@@ -64,7 +64,12 @@ def gather_rows(local_block, plan: ShardPlan, out=None, group=None):
         out = torch.empty((plan.world,) + tuple(local_block.shape), dtype=local_block.dtype,
                           device=local_block.device)
     if dist.get_backend(group) == "gloo":
-        dist.all_gather(list(out.unbind(0)), local_block, group=group)
+        if local_block.is_cuda:  # rehearsal of the GPU path over gloo: stage through the host
+            host = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather(list(host.unbind(0)), local_block.cpu(), group=group)
+            out.copy_(host)
+        else:
+            dist.all_gather(list(out.unbind(0)), local_block, group=group)
     else:
         dist.all_gather_into_tensor(out, local_block, group=group)
     return out
