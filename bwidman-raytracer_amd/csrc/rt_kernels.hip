@@ -921,6 +921,7 @@ rt_render_kernel(rt_kparams K) {
 #undef STAMP
 }
 
+#ifndef RT_TU_BVH  // defined once, in the main translation unit
 // initializeRand (Main.cu:369-380): curand_init(y*W + x, 0, 0)
 __global__ void __launch_bounds__(256) rt_init_rand_kernel(unsigned* rng, int width, int rows,
                                                            int row_offset, int row_stride) {
@@ -956,6 +957,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
     const int j = y / shards;
     image[q] = gathered[((long)r * rows_per_shard + j) * width + x];
 }
+#endif  // RT_TU_BVH
 
 
 // ===========================================================================
@@ -1341,10 +1343,32 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
     return hipGetLastError();
 }
 
+}  // namespace
+
+#ifdef RT_TU_BVH
+// The BVH instantiations live in their own translation unit
+// (rt_kernels_bvh.hip), built at -O3: the traversal loops want the full
+// optimizer while the brute-force kernels are faster at -O1.
+hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
+                                hipStream_t s) {
+    if (block == 64)
+        return sorted ? launch_render<64, false, true, true>(K, lds, grid_mult, num_cus, s)
+                      : launch_render<64, false, false, true>(K, lds, grid_mult, num_cus, s);
+    if (block == 128)
+        return sorted ? launch_render<128, false, true, true>(K, lds, grid_mult, num_cus, s)
+                      : launch_render<128, false, false, true>(K, lds, grid_mult, num_cus, s);
+    return sorted ? launch_render<256, false, true, true>(K, lds, grid_mult, num_cus, s)
+                  : launch_render<256, false, false, true>(K, lds, grid_mult, num_cus, s);
+}
+#else
+hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
+                                hipStream_t s);
+
+namespace {
 template <int BLOCK, bool SORTED>
 hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s) {
     if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
-        return launch_render<BLOCK, false, SORTED, true>(K, lds, grid_mult, num_cus, s);
+        return rt_launch_render_bvh(K, BLOCK, SORTED, lds, grid_mult, num_cus, s);
     return hit_lds ? launch_render<BLOCK, true, SORTED, false>(K, lds, grid_mult, num_cus, s)
                    : launch_render<BLOCK, false, SORTED, false>(K, lds, grid_mult, num_cus, s);
 }
@@ -1415,3 +1439,4 @@ hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int
                        width, height, shards, rows_per_shard);
     return hipGetLastError();
 }
+#endif  // RT_TU_BVH

@@ -6,8 +6,13 @@ cd "$(dirname "$0")/../bwidman-raytracer_amd"
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   out=build/variants/$name; mkdir -p $out
+  /opt/rocm/bin/hipcc -O1 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -fno-unroll-loops -fvisibility=hidden ${TUNE:--DRT_WAVES_PER_EU=6 -DRT_SORTED_BLOCK=256} $flags \
+     -c -o $out/k.o csrc/rt_kernels.hip
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -fno-unroll-loops -fvisibility=hidden ${TUNE:--DRT_WAVES_PER_EU=6 -DRT_SORTED_BLOCK=256} $flags \
-     -shared -Wl,-rpath,/opt/rocm/lib -o $out/libbwrt.so csrc/rt_kernels.hip -x hip csrc/rt_context.cpp
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -fno-unroll-loops $flags --cuda-device-only -c \
+     -c -o $out/kb.o csrc/rt_kernels_bvh.hip
+  /opt/rocm/bin/hipcc -O1 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fvisibility=hidden ${TUNE:--DRT_WAVES_PER_EU=6 -DRT_SORTED_BLOCK=256} $flags \
+     -x hip -c -o $out/c.o csrc/rt_context.cpp
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -Wl,-rpath,/opt/rocm/lib -o $out/libbwrt.so $out/k.o $out/kb.o $out/c.o
+  /opt/rocm/bin/hipcc -O1 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -fno-unroll-loops $flags --cuda-device-only -c \
      -Rpass-analysis=kernel-resource-usage -o /dev/null csrc/rt_kernels.hip 2>&1 | grep -A2 "rt_render_kernelILi256ELb1" | grep -E "VGPRs:|SGPRs" | sed "s/^/$name: /" || true
 done
