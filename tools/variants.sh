@@ -9,7 +9,7 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc -O1 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -fno-unroll-loops -fvisibility=hidden ${TUNE:--DRT_WAVES_PER_EU=6 -DRT_SORTED_BLOCK=256} $flags \
      -c -o $out/k.o csrc/rt_kernels.hip
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -fno-unroll-loops -fvisibility=hidden ${TUNE:--DRT_WAVES_PER_EU=6 -DRT_SORTED_BLOCK=256} $flags \
-     -c -o $out/kb.o csrc/rt_kernels_bvh.hip
+     ${BVHFLAGS:--URT_WAVES_PER_EU -DRT_WAVES_PER_EU=4} -c -o $out/kb.o csrc/rt_kernels_bvh.hip
   /opt/rocm/bin/hipcc -O1 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fvisibility=hidden ${TUNE:--DRT_WAVES_PER_EU=6 -DRT_SORTED_BLOCK=256} $flags \
      -x hip -c -o $out/c.o csrc/rt_context.cpp
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -Wl,-rpath,/opt/rocm/lib -o $out/libbwrt.so $out/k.o $out/kb.o $out/c.o
