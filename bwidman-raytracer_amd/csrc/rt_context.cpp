@@ -590,10 +590,29 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             B.finish();
             c->bvh_nodes_per_order = B.n_nodes;
             off_bvh = (total + 3) & ~(size_t)3;
-            off_bvh_prims = off_bvh + B.nodes.size();
-            h.resize(off_bvh_prims + B.prims.size() + 4, 0.0f);
+            off_bvh_prims = off_bvh + B.nodes.size();  // leaf records, RT_LEAF_FLOATS each
+            h.resize(off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS + 4, 0.0f);
             std::memcpy(h.data() + off_bvh, B.nodes.data(), B.nodes.size() * sizeof(float));
-            std::memcpy(h.data() + off_bvh_prims, B.prims.data(), B.prims.size() * sizeof(int));
+            for (size_t j = 0; j < B.prims.size(); j++) {
+                const int id = B.prims[j];
+                float* r = h.data() + off_bvh_prims + j * RT_LEAF_FLOATS;
+                int kind, idx, nf;
+                const float* src;
+                if (id < ns) {
+                    kind = 0, idx = id, nf = RT_SPH_FLOATS, src = h.data() + (size_t)idx * RT_SPH_FLOATS;
+                } else if (id < ns + np + nt) {
+                    kind = 2, idx = id - ns - np, nf = RT_TRI_FLOATS, src = h.data() + off_tri + (size_t)idx * RT_TRI_FLOATS;
+                } else {
+                    kind = 3, idx = id - ns - np - nt, nf = RT_QUAD_FLOATS,
+                    src = h.data() + off_quad + (size_t)idx * RT_QUAD_FLOATS;
+                }
+                const int key = RT_KEY(kind, idx), zero = 0;
+                std::memcpy(&r[0], &id, 4);
+                std::memcpy(&r[1], &key, 4);
+                std::memcpy(&r[2], &kind, 4);
+                std::memcpy(&r[3], &zero, 4);
+                std::memcpy(&r[4], src, (size_t)nf * sizeof(float));
+            }
         }
     }
     const size_t bytes = h.size() * sizeof(float);
@@ -824,7 +843,7 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.quad = base + c->off_quad;
     K.hit = base + c->off_hit;
     K.bvh_nodes = c->off_bvh ? base + c->off_bvh : nullptr;
-    K.bvh_prims = c->off_bvh ? reinterpret_cast<const int*>(base + c->off_bvh_prims) : nullptr;
+    K.bvh_leafrec = c->off_bvh ? base + c->off_bvh_prims : nullptr;
     K.rng = (unsigned*)c->rng.p;
     K.accum = (float*)c->accum.p;
     return RT_OK;

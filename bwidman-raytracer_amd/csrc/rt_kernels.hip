@@ -407,6 +407,54 @@ __device__ __forceinline__ bool key_accept(float t, int key, float best_t, int b
     return !(t <= RT_NEAR_ZERO) && (t < best_t || (t == best_t && key > best_key));
 }
 
+// Leaf record (rt_layout.h RT_LEAF_FLOATS): {id, key, kind, 0, record...};
+// the header and the first record float4 are loaded together (no dependent
+// index load in the leaf loop).
+__device__ __forceinline__ void leaf_test(const float* r, f3 o, f3 d, float a2, float a4, float& best_t, int& best_id,
+                                          int& best_key) {
+    const float4 h = *reinterpret_cast<const float4*>(r);
+    const float4 a = *reinterpret_cast<const float4*>(r + 4);
+    const int id = __float_as_int(h.x), key = __float_as_int(h.y), kind = __float_as_int(h.z);
+    if (kind == 0) {  // sphere {c, r^2}, Intersection.cuh:15-62
+        const f3 xp = mk(o.x - a.x, o.y - a.y, o.z - a.z);
+        const float b = 2.0f * dot(xp, d);
+        const float c = dot(xp, xp) - a.w;
+        const float disc = b * b - a4 * c;
+        if (!(disc < 0.0f) && !(b >= 0.0f)) {
+            const float t = (-b - sqrtf(disc)) / a2;
+            if (key_accept(t, key, best_t, best_key)) {
+                best_t = t;
+                best_id = id;
+                best_key = key;
+            }
+        }
+        return;
+    }
+    const float* q = r + 4;  // triangle / quad record {n, d, (v_k, in_k)...}
+    const float nd = a.x * d.x + a.y * d.y + a.z * d.z;
+    if (fabsf(nd) < RT_NEAR_ZERO) return;
+    const float t = -((a.x * o.x + a.y * o.y + a.z * o.z) + a.w) / nd;
+    if (!key_accept(t, key, best_t, best_key)) return;
+    const f3 P = add(o, scale(t, d));
+    const float4 e0 = *reinterpret_cast<const float4*>(q + 4);
+    const float4 e1 = *reinterpret_cast<const float4*>(q + 8);
+    const float4 e2 = *reinterpret_cast<const float4*>(q + 12);
+    const float4 e3 = *reinterpret_cast<const float4*>(q + 16);
+    const float4 e4 = *reinterpret_cast<const float4*>(q + 20);
+    bool inside = !(dot(mk(e0.w, e1.x, e1.y), sub(P, mk(e0.x, e0.y, e0.z))) < 0.0f) &&
+                  !(dot(mk(e2.y, e2.z, e2.w), sub(P, mk(e1.z, e1.w, e2.x))) < 0.0f) &&
+                  !(dot(mk(e3.w, e4.x, e4.y), sub(P, mk(e3.x, e3.y, e3.z))) < 0.0f);
+    if (kind == 3 && inside) {
+        const float4 e5 = *reinterpret_cast<const float4*>(q + 24);
+        inside = !(dot(mk(e5.y, e5.z, e5.w), sub(P, mk(e4.z, e4.w, e5.x))) < 0.0f);
+    }
+    if (inside) {
+        best_t = t;
+        best_id = id;
+        best_key = key;
+    }
+}
+
 __device__ __forceinline__ void prim_test(const rt_kparams& K, int id, f3 o, f3 d, float a2, float a4, float& best_t,
                                           int& best_id, int& best_key) {
     const int ns = K.n_sph, tri_base = K.n_sph + K.n_pln, quad_base = tri_base + K.n_tri;
@@ -534,7 +582,8 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
             const int first = leaf & 0xffffff, count = leaf >> 24;
             for (int k = 0; k < count; k++) {
                 RT_BRANCH_COUNT(K, 6);
-                prim_test(K, K.bvh_prims[first + k], o, d, a2, a4, best_t, best_id, best_key);
+                leaf_test(K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
+                          best_key);
             }
         }
     }

@@ -34,6 +34,7 @@
 #define RT_QUAD_FLOATS 32
 #define RT_TRI_CULL 24   // offset of the cull sphere in a triangle record
 #define RT_QUAD_CULL 28
+#define RT_LEAF_FLOATS 36  // BVH leaf record: 4 header + up to 32 record floats
 #define RT_HIT_FLOATS 12
 
 #define RT_NEAR_ZERO 0.0001f       // Intersection.cuh:4
@@ -69,9 +70,10 @@ struct rt_kparams {
     // floats {bmin.xyz, miss, bmax.xyz, leaf}, depth-first (first child =
     // node + 1, near side of the split first for that octant), miss = next node when
     // the subtree is skipped (-1 = done), leaf = -1 (internal) or
-    // (count << 24) | first index into bvh_prims (global primitive ids).
+    // (count << 24) | first index into bvh_leafrec: {id, RT_KEY, kind (0
+    // sphere, 2 triangle, 3 quad), 0, then the compiled record}.
     const float* bvh_nodes;
-    const int* bvh_prims;
+    const float* bvh_leafrec;   // leaf records in leaf order, RT_LEAF_FLOATS each
     int bvh_order_stride;
     // conservative polygon culling (see polygon_test): only rays whose origin
     // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
