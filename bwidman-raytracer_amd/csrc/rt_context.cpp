@@ -139,15 +139,23 @@ int shard_rows(int height, int row_offset, int row_stride) {
 }
 
 void put_material(float* h, const rt_material& m) {
-    h[4] = m.albedo.x;
-    h[5] = m.albedo.y;
-    h[6] = m.albedo.z;
-    h[7] = m.emittance;
+    // emittedLight = emittance * albedo (Main.cu:238)
+    h[4] = m.emittance * m.albedo.x;
+    h[5] = m.emittance * m.albedo.y;
+    h[6] = m.emittance * m.albedo.z;
+    h[7] = 0.0f;
     h[8] = m.roughness;
     // fresnel(): square(ior)/square(1.0f) - 1.0f (Main.cu:125)
     h[9] = (m.refractive_index * m.refractive_index) / (1.0f * 1.0f) - 1.0f;
     h[10] = m.roughness * m.roughness;  // Main.cu:119 evaluates roughness*roughness first
     h[11] = 0.0f;
+    // diffuse brdf = 2 / (1 - specularChance) * albedo (Main.cu:259): the
+    // double constant narrows to 4.0f; scaling by 4 is exact
+    const float dk = (float)(2.0 / (1 - 0.5f));
+    h[12] = dk * m.albedo.x;
+    h[13] = dk * m.albedo.y;
+    h[14] = dk * m.albedo.z;
+    h[15] = 0.0f;
 }
 
 // Triangle / quad record: {n, d, v0, in0, v1, in1, ...}; Intersection.cuh:109-127

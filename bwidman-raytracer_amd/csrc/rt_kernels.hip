@@ -744,14 +744,17 @@ __device__ __forceinline__ f3 specular_scatter(Xorwow& rs, f3 d, f3 n, float rou
 //   brdf = kspec * {1,1,1} (specular) or 4 * albedo (diffuse, :259).
 __device__ __forceinline__ void fold_level(int c0, float k, float c, const float* hit_tab, float& lx, float& ly,
                                            float& lz) {
+    // hit table (rt_context.cpp put_material): [4..6] emitted = emittance *
+    // albedo, [12..14] diffuse brdf = (2/(1-specularChance)) * albedo, both
+    // formed on the host with the same single float multiplications
     const bool spec = c0 < 0;
-    const float4 mat = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * (spec ? ~c0 : c0) + 4);
-    const float ex = mat.w * mat.x, ey = mat.w * mat.y, ez = mat.w * mat.z;
-    const float dk = (float)(2.0 / (1 - RT_SPECULAR_CHANCE));  // 4.0f
-    const float bx = spec ? k : dk * mat.x, by = spec ? k : dk * mat.y, bz = spec ? k : dk * mat.z;
-    lx = ex + (bx * lx) * c;
-    ly = ey + (by * ly) * c;
-    lz = ez + (bz * lz) * c;
+    const float* h = hit_tab + RT_HIT_FLOATS * (spec ? ~c0 : c0);
+    const float4 e = *reinterpret_cast<const float4*>(h + 4);
+    const float4 da = *reinterpret_cast<const float4*>(h + 12);
+    const float bx = spec ? k : da.x, by = spec ? k : da.y, bz = spec ? k : da.z;
+    lx = e.x + (bx * lx) * c;
+    ly = e.y + (by * ly) * c;
+    lz = e.z + (bz * lz) * c;
 }
 
 // Folds levels depth-1 .. 0 of the LDS record stack into L (in/out).
@@ -930,19 +933,8 @@ rt_render_kernel(rt_kparams K) {
                 // (4) fold the recursion innermost-first (Main.cu:262-268):
                 //     L = emitted + (brdf * L) * cosAngle
                 float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor
-                for (int l = depth - 1; l >= 0; --l) {
-                    const int c0 = rec_code[l * BLOCK];
-                    const float k = rec_k[l * BLOCK];
-                    const float c = rec_c[l * BLOCK];
-                    const bool spec = c0 < 0;
-                    const float4 mat = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * (spec ? ~c0 : c0) + 4);
-                    const float ex = mat.w * mat.x, ey = mat.w * mat.y, ez = mat.w * mat.z;  // emittance * albedo
-                    const float dk = (float)(2.0 / (1 - RT_SPECULAR_CHANCE));                 // 4.0f
-                    const float bx = spec ? k : dk * mat.x, by = spec ? k : dk * mat.y, bz = spec ? k : dk * mat.z;
-                    lx = ex + (bx * lx) * c;
-                    ly = ey + (by * ly) * c;
-                    lz = ez + (bz * lz) * c;
-                }
+                for (int l = depth - 1; l >= 0; --l)
+                    fold_level(rec_code[l * BLOCK], rec_k[l * BLOCK], rec_c[l * BLOCK], hit_tab, lx, ly, lz);
                 // (5) progressive accumulation (Main.cu:299-304), spp = 1
                 if (px.frame == 1u) {
                     px.ax = 0.0f;

@@ -15,9 +15,10 @@
 //   triangles : n_tri  x 28 floats  {nx,ny,nz,d, v0[3],in0[3], v1[3],in1[3], v2[3],in2[3], pad2,
 //                                    cull sphere {cx,cy,cz,Rc^2}}
 //   quads     : n_quad x 32 floats  {nx,ny,nz,d, v0[3],in0[3], .. v3[3],in3[3], cull {.., Rc^2 = inf}}
-//   hit table : n_prim x 12 floats  {n_or_centre[3], is_sphere,
-//                                    albedo[3], emittance,
-//                                    roughness, ior^2-1, 0, 0}
+//   hit table : n_prim x 16 floats  {n_or_centre[3], is_sphere,
+//                                    emittance*albedo[3], 0,
+//                                    roughness, ior^2-1, roughness^2, 0,
+//                                    4*albedo[3], 0}
 //   primitive id = index within its kind + kind offset, kinds ordered
 //   spheres, planes, triangles, quads.
 //
@@ -35,7 +36,7 @@
 #define RT_TRI_CULL 24   // offset of the cull sphere in a triangle record
 #define RT_QUAD_CULL 28
 #define RT_LEAF_FLOATS 36  // BVH leaf record: 4 header + up to 32 record floats
-#define RT_HIT_FLOATS 12
+#define RT_HIT_FLOATS 16
 
 #define RT_NEAR_ZERO 0.0001f       // Intersection.cuh:4
 #define RT_SPECULAR_CHANCE 0.5f    // Main.cu:29
