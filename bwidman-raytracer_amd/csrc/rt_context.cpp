@@ -81,6 +81,7 @@ struct rt_context {
     float cull_omax = 0.0f;  // polygon culling bound (rt_layout.h)
     float background[3] = {0.0f, 0.0f, 0.0f};  // backgroundColor, Main.cu:27
     int bvh_nodes_per_order = 0;
+    int bvh_order_mask = 7;
     DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table | bvh nodes | bvh prims
     size_t off_bvh = 0, off_bvh_prims = 0;  // in floats; 0 = no BVH
     size_t off_pln = 0, off_tri = 0, off_quad = 0, off_hit = 0;  // in floats
@@ -264,6 +265,7 @@ struct BvhBuilder {
     static constexpr int kBins = 16;
     int max_leaf = 8;         // BWRT_BVH_LEAF
     float trav_cost = 0.0f;   // BWRT_BVH_CT: SAH cost of one node step relative to one primitive test
+    int order_mask = 7;       // BWRT_BVH_ORDER_MASK: octant bits that get their own node array
     std::vector<BvhItem> items;
     std::vector<BvhNode> tree;
     std::vector<int> prims;
@@ -396,6 +398,7 @@ struct BvhBuilder {
         nodes.assign((size_t)8 * n_nodes * 8, 0.0f);
         std::vector<int> pos(n_nodes), seq, end(n_nodes);
         for (int order = 0; order < 8; order++) {
+            if (order & ~order_mask) continue;  // never selected by the kernel
             seq.clear();
             emit(order, 0, pos, seq);
             // subtree end in this order: position after the last descendant
@@ -594,9 +597,11 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             B.tree.reserve(2 * (size_t)nb);
             if (const char* e = std::getenv("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 255);
             if (const char* e = std::getenv("BWRT_BVH_CT")) B.trav_cost = (float)std::atof(e);
+            if (const char* e = std::getenv("BWRT_BVH_ORDER_MASK")) B.order_mask = std::atoi(e) & 7;
             B.build(0, nb);
             B.finish();
             c->bvh_nodes_per_order = B.n_nodes;
+            c->bvh_order_mask = B.order_mask;
             off_bvh = (total + 3) & ~(size_t)3;
             off_bvh_prims = off_bvh + B.nodes.size();  // leaf records, RT_LEAF_FLOATS each
             h.resize(off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS + 4, 0.0f);
@@ -839,6 +844,7 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.n_quad = c->n_quad;
     K.cull_omax = c->cull_omax;
     K.bvh_order_stride = c->bvh_nodes_per_order * 8;
+    K.bvh_order_mask = c->bvh_order_mask;
     int nmax = c->n_sph;  // Main.cu:217
     if (c->n_pln > nmax) nmax = c->n_pln;
     if (c->n_tri > nmax) nmax = c->n_tri;

@@ -538,7 +538,7 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
                      fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z);
     const f3 inv = mk(1.0f / dc.x, 1.0f / dc.y, 1.0f / dc.z);
     // node array of the ray's direction octant (near children first)
-    const int order = (d.x < 0.0f) | ((d.y < 0.0f) << 1) | ((d.z < 0.0f) << 2);
+    const int order = ((d.x < 0.0f) | ((d.y < 0.0f) << 1) | ((d.z < 0.0f) << 2)) & K.bvh_order_mask;
     const float* nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
     // speculative while-while traversal (Aila & Laine): a lane that reaches a
     // leaf its ray enters parks it and walks on; the parked leaves are tested

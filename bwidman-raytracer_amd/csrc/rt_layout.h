@@ -76,6 +76,7 @@ struct rt_kparams {
     const float* bvh_nodes;
     const float* bvh_leafrec;   // leaf records in leaf order, RT_LEAF_FLOATS each
     int bvh_order_stride;
+    int bvh_order_mask;         // octant bits with their own arrays (7 = all three axes)
     // conservative polygon culling (see polygon_test): only rays whose origin
     // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
     float cull_omax;
