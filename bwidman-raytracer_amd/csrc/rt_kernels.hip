@@ -1145,7 +1145,6 @@ rt_render_sorted_kernel(rt_kparams K) {
 #define RES(f, i) slots[((f) < 4 ? (f) : (f) + 3) * BLOCK + (i)]
 #endif
 
-    const long T = (long)gridDim.x * BLOCK;
     PixelState px;
     load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
     int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
@@ -1174,13 +1173,9 @@ rt_render_sorted_kernel(rt_kparams K) {
         px.az = px.az + lz;
         px.frame++;
         px.passes_left--;
-        // a finished pixel is stored here only if the lane has another one to
-        // render (persistent grids); otherwise after the loop, by the whole
-        // wave at once
-        if (px.passes_left == 0 && px.w + T < nitems) {
-            store_pixel(K, npix, px);
-            load_item(K, npix, nitems, px.w + T, px);
-        }
+        // one pixel per lane (the grid covers every work item): a finished
+        // pixel is stored after the loop, by the whole wave at once, and the
+        // camera set-up constants are not live inside the loop
         mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
     };
     bool ended = false;  // path ended this round: finish_path() once, after the I-phase
@@ -1442,7 +1437,7 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
         nitems = tiles_x * tiles_y * 64;
     }
     long grid = (nitems + BLOCK - 1) / BLOCK;  // streaming needs a resident grid only
-    if (grid_mult > 0) {  // persistent: grid_mult x resident workgroups per CU x CUs
+    if (grid_mult > 0 && !SORTED) {  // persistent (simple kernel): grid_mult x resident groups per CU x CUs
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH>(), BLOCK, lds) ==
                 hipSuccess &&
@@ -1508,8 +1503,9 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 
 // Host-side launch policy: 256-lane workgroups (64 when the record stack of
 // very deep paths would not fit), hit table in LDS when it fits in 16 KB,
-// sorted task-queue kernel unless `simple`; grid_mult > 0 caps the grid at
-// grid_mult x resident workgroups per CU (persistent lanes).
+// sorted task-queue kernel unless `simple` (one pixel per lane: its grid
+// always covers every item); for the simple kernel grid_mult > 0 caps the
+// grid at grid_mult x resident workgroups per CU (persistent lanes).
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, hipStream_t stream) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = !K.bvh_nodes && (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
