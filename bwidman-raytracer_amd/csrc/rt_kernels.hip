@@ -242,6 +242,30 @@ __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters 
     return r;
 }
 
+#ifdef RT_REJ_CAP
+// At most RT_REJ_CAP rejection trips per round: a task still rejecting is
+// handed back with its advanced RNG state and re-posted next round (the
+// candidate stream is memoryless in the state, so the accepted point is the
+// same one).  Returns false when not yet accepted.
+__device__ __forceinline__ bool random_direction_capped(Xorwow& s, f3 normal, f3& out) {
+    f3 r;
+    int trips = 0;
+    bool ok;
+    do {
+        float x = rand_pm1(s);
+        float y = rand_pm1(s);
+        float z = rand_pm1(s);
+        r = mk(x, y, z);
+        ok = !(r.x * r.x + r.y * r.y + r.z * r.z > 1.00000012f);
+    } while (!ok && ++trips < RT_REJ_CAP);
+    if (!ok) return false;
+    r = normalize3(r);
+    if (dot(normal, r) < 0.0f) r = sub(r, scale(2.0f * dot(r, normal), normal));
+    out = r;
+    return true;
+}
+#endif
+
 // ---- closest hit over the whole scene (Main.cu:217-234 + Intersection.cuh)
 // The loop index is wave-uniform: primitive fields are scalar loads.  Only
 // (t, primitive id) of the running closest hit are tracked; the hit point
@@ -1289,8 +1313,15 @@ rt_render_sorted_kernel(rt_kparams K) {
                 int* rej_ptr = nullptr;
 #endif
                 if (do_front) {
+#ifdef RT_REJ_CAP
+                    (void)rej_ptr;
+                    const bool done = random_direction_capped(rs, nrm, r);
+                    if (done && code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // Main.cu:291-292
+                    RES(3, tid) = done ? 0.0f : 1.0f;  // 1: still rejecting, re-post
+#else
                     r = random_direction(rs, nrm, rej_ptr);
                     if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
+#endif
                 } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
@@ -1345,6 +1376,12 @@ rt_render_sorted_kernel(rt_kparams K) {
             px.rs.v2 = __float_as_uint(RES(7, slot));
             px.rs.v3 = __float_as_uint(RES(8, slot));
             px.rs.v4 = __float_as_uint(RES(9, slot));
+#ifdef RT_REJ_CAP
+            if (task != T_SPEC && RES(3, slot) != 0.0f) {
+                // rejection sampling not finished: same task again next round
+            } else
+#endif
+            {
             mode = M_IDLE;
             if (task == T_REGEN) {
                 o = cam;
@@ -1369,6 +1406,7 @@ rt_render_sorted_kernel(rt_kparams K) {
                     ended = true;
                 }
                 depth++;
+            }
             }
         }
 
