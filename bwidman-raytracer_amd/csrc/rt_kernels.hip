@@ -637,6 +637,10 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
     const f3 dc = mk(fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x, fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y,
                      fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z);
     const f3 inv = mk(1.0f / dc.x, 1.0f / dc.y, 1.0f / dc.z);
+    // slab distances as fma(b, inv, -o*inv): the rounding of o*inv (at most
+    // 2^-24 |o*inv| per axis) is covered by the absolute margin `m`
+    const f3 oinv = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+    const float m = 1e-6f + 9.5367431640625e-07f * fmaxf(fmaxf(fabsf(oinv.x), fabsf(oinv.y)), fabsf(oinv.z));
     // node array of the ray's direction octant (near children first)
     const int order = ((d.x < 0.0f) | ((d.y < 0.0f) << 1) | ((d.z < 0.0f) << 2)) & K.bvh_order_mask;
     const float* nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
@@ -654,14 +658,14 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
                 RT_BRANCH_COUNT(K, 5);
                 const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
                 const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
-                const float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
-                const float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
-                const float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+                const float tx0 = __builtin_fmaf(lo.x, inv.x, -oinv.x), tx1 = __builtin_fmaf(hi.x, inv.x, -oinv.x);
+                const float ty0 = __builtin_fmaf(lo.y, inv.y, -oinv.y), ty1 = __builtin_fmaf(hi.y, inv.y, -oinv.y);
+                const float tz0 = __builtin_fmaf(lo.z, inv.z, -oinv.z), tz1 = __builtin_fmaf(hi.z, inv.z, -oinv.z);
                 const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
                 const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-                // margins: 1e-5 relative + 1e-6 absolute on the interval, and prune
-                // against the current closest distance only beyond the same margin
-                const bool hit = tmin <= tmax * (1.0f + 1e-5f) + 1e-6f && tmin <= best_t * (1.0f + 1e-5f) + 1e-5f;
+                // margins: 1e-5 relative + m absolute on the interval, and prune
+                // against the current closest distance only beyond the same margins
+                const bool hit = tmin <= tmax * (1.0f + 1e-5f) + m && tmin <= best_t * (1.0f + 1e-5f) + (1e-5f + m);
                 const int miss = __float_as_int(lo.w);
                 const int lf = __float_as_int(hi.w);
                 if (!hit) {
