@@ -5,6 +5,6 @@ The product is the HIP library bwidman-raytracer_amd/lib/libbwrt.so
 reference's driver (scenes, render loop, multi-GPU sharding).
 """
 from . import abi, scenes  # noqa: F401
-from .renderer import Renderer, shard_rows  # noqa: F401
+from .renderer import Renderer, render_multi, shard_rows  # noqa: F401
 
-__all__ = ["abi", "scenes", "Renderer", "shard_rows"]
+__all__ = ["abi", "scenes", "Renderer", "render_multi", "shard_rows"]

@@ -140,3 +140,16 @@ class Renderer:
 
 def shard_rows(height: int, row_offset: int, row_stride: int) -> int:
     return len(range(row_offset, height, row_stride)) if row_stride > 0 else 0
+
+
+def render_multi(renderers, width: int, height: int, samples: int) -> np.ndarray:
+    """rt_render_multi: one image across several Renderers (one per GPU, same
+    scene/camera set on each) in this process; returns (H, W, 4) uint8, row 0
+    = bottom.  Renderer i renders rows y = i (mod len(renderers))."""
+    lib = renderers[0].lib
+    arr = (C.c_void_p * len(renderers))(*[r.ctx.value for r in renderers])
+    out = np.empty((height, width, 4), np.uint8)
+    rc = lib.rt_render_multi(arr, len(renderers), width, height, samples, out.ctypes.data)
+    if rc != abi.RT_OK:
+        renderers[0]._check(rc)
+    return out

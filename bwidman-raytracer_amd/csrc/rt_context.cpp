@@ -89,6 +89,8 @@ struct rt_context {
     // shard state
     int width = 0, height = 0, row_offset = 0, row_stride = 1, rows = 0;
     DevBuf rng, accum, rgba;
+    void* host_rgba = nullptr;  // pinned staging for rt_render_multi
+    size_t host_rgba_bytes = 0;
     int tile_w = 16;             // BWRT_TILE: wave tile width (16 x 4 pixel waves; 0 = linear order)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
@@ -491,6 +493,7 @@ void rt_destroy(rt_context* c) {
     free_buf(c->rng);
     free_buf(c->accum);
     free_buf(c->rgba);
+    if (c->host_rgba) (void)hipHostFree(c->host_rgba);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -926,6 +929,59 @@ int rt_render(rt_context* c, int width, int height, int samples, uint8_t* rgba_o
     p.row_offset = 0;
     p.row_stride = 1;
     return rt_render_ex(c, &p, rgba_out, nullptr);
+}
+
+// Single-process multi-GPU (the C++ host's counterpart of bench.py's one
+// process per GPU): context i renders rows y = i (mod n) on its own stream,
+// all launches in flight at once; the shards come back through pinned host
+// buffers and are interleaved on the host.
+int rt_render_multi(rt_context* const* ctxs, int n, int width, int height, int samples, uint8_t* rgba_out) {
+    if (!ctxs || n <= 0 || width <= 0 || height <= 0 || samples <= 0) return RT_ERR_INVALID_ARGUMENT;
+    for (int i = 0; i < n; i++) {
+        if (!ctxs[i]) return RT_ERR_INVALID_ARGUMENT;
+        for (int j = 0; j < i; j++)
+            if (ctxs[j] == ctxs[i]) return fail(ctxs[i], RT_ERR_INVALID_ARGUMENT, "context listed twice");
+    }
+    const int active = n < height ? n : height;  // contexts beyond the image height get no rows
+    for (int i = 0; i < active; i++) {
+        rt_context* c = ctxs[i];
+        rt_render_params p;
+        p.width = width;
+        p.height = height;
+        p.samples = samples;
+        p.max_bounces = c->max_bounces;
+        p.first_frame = 0;
+        p.row_offset = i;
+        p.row_stride = n;
+        rt_kparams K;
+        unsigned first = 0;
+        int rc = prepare(c, &p, K, first);
+        if (rc) return rc;
+        const size_t bytes = (size_t)c->rows * width * 4;
+        rc = ensure_buf(c, c->rgba, bytes);
+        if (rc) return rc;
+        if (c->host_rgba_bytes < bytes) {
+            if (c->host_rgba) (void)hipHostFree(c->host_rgba);
+            c->host_rgba = nullptr;
+            c->host_rgba_bytes = 0;
+            HIP_TRY(c, hipHostMalloc(&c->host_rgba, bytes, hipHostMallocDefault));
+            c->host_rgba_bytes = bytes;
+        }
+        K.rgba = (unsigned*)c->rgba.p;
+        rc = launch(c, K, c->stream, first, samples);
+        if (rc) return rc;
+        HIP_TRY(c, hipMemcpyAsync(c->host_rgba, c->rgba.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    }
+    for (int i = 0; i < active; i++) {
+        rt_context* c = ctxs[i];
+        HIP_TRY(c, hipSetDevice(c->device));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (!rgba_out) continue;
+        const uint8_t* src = (const uint8_t*)c->host_rgba;
+        for (int j = 0; j < c->rows; j++)
+            std::memcpy(rgba_out + ((size_t)(i + j * n) * width) * 4, src + (size_t)j * width * 4, (size_t)width * 4);
+    }
+    return RT_OK;
 }
 
 int rt_render_device(rt_context* c, const rt_render_params* p, void* rgba_device, void* stream) {

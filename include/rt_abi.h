@@ -249,6 +249,17 @@ RT_API int rt_render_device(rt_context* ctx, const rt_render_params* p,
  * to rt_render_device). */
 RT_API int rt_synchronize(rt_context* ctx);
 
+/* One image across n contexts in ONE process (one context per GPU, the same
+ * scene / camera / max_bounces set on each; the C++ host's multi-GPU path,
+ * SURVEY §8e): context i renders rows y = i (mod n) of the frames that
+ * continue its own frame counter, all contexts concurrently on their own
+ * streams; the RGBA8 rows are gathered into rgba_out (host, width*height*4,
+ * row 0 = bottom; may be NULL).  Keep the contexts' frame counters in step by
+ * always rendering them together.  Equal to one context rendering the whole
+ * image (tests/test_gpu_parity.py). */
+RT_API int rt_render_multi(rt_context* const* ctxs, int n, int width, int height, int samples,
+                           uint8_t* rgba_out);
+
 /* Duration (ms, HIP events on the launch stream) of the last render kernel
  * launch; -1 when unavailable.  Synchronises on that launch's end event. */
 RT_API float rt_last_kernel_ms(rt_context* ctx);

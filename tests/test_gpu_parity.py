@@ -376,3 +376,28 @@ def test_repeated_renders_are_identical(gpu, oracle):
             img = gpu.render(w, h, spp, mb, first_frame=1)
             assert np.array_equal(img, st.rgba)
             same_state(gpu, st)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_render_multi_contexts(bwrt_lib, oracle, n):
+    """rt_render_multi (single-process multi-GPU for C++ hosts): n contexts —
+    here all on device 0, as a rehearsal of n GPUs — each render rows
+    y = i (mod n) concurrently; the gathered frames equal the oracle's, for
+    two successive calls (frame counters continue in step)."""
+    from bwrt import Renderer, render_multi
+    s = scenes.scene_07()
+    rs = [Renderer(0, lib=bwrt_lib) for _ in range(n)]
+    try:
+        for i, r in enumerate(rs):
+            r.set_scene(s)
+            r.set_max_bounces(4)
+            r.init_rand(320, 181, i, n)
+        st = oracle.OracleState(320, 181)
+        for call in range(2):
+            img = render_multi(rs, 320, 181, 2)
+            oracle.render(s, st, 2, 4, first_frame=1 if call == 0 else None)
+            assert np.array_equal(img, st.rgba), f"call {call}"
+        assert all(r.frame_counter == 5 for r in rs)
+    finally:
+        for r in rs:
+            r.close()
