@@ -8,14 +8,15 @@
 //
 //   bwrt_render [--scene 07|01|04|04_box | --scene-file FILE] [--save-scene FILE]
 //               [--width 1920] [--height 1080] [--frames 8] [--frames-per-call 1]
-//               [--max-bounces 5] [--background r,g,b] [--device 0]
+//               [--max-bounces 5] [--background r,g,b] [--device 0] [--gpus 1]
 //               [--keys "W*10,W+LEFT*5,*3"] [--dt SECONDS]
 //               [--out image.png|image.ppm] [--dump-scene file.bin]
 //
 // --keys: comma-separated steps KEY[+KEY...]*FRAMES (keys W A S D SPACE
 // LEFT_SHIFT LEFT RIGHT UP DOWN ESCAPE; an empty key list holds nothing);
 // the timeline repeats its last step.  ESCAPE ends the loop like
-// glfwSetWindowShouldClose.
+// glfwSetWindowShouldClose.  --gpus N renders every frame across N contexts
+// (devices device..device+N-1, modulo the visible count) with rt_render_multi.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -86,6 +87,7 @@ static bool parse_keys(const std::string& spec, std::vector<KeyStep>& steps) {
 int main(int argc, char** argv) {
     std::string scene_name = "07", scene_file, save, out, dump, keys_spec;
     int width = 1920, height = 1080, frames = 8, per_call = 1, max_bounces = RT_DEFAULT_MAX_BOUNCES, device = 0;
+    int gpus = 1;
     float bg[3] = {0.0f, 0.0f, 0.0f};
     double fixed_dt = -1.0;
     for (int i = 1; i < argc; i++) {
@@ -150,13 +152,18 @@ int main(int argc, char** argv) {
     }
     if (!dump.empty() || (!save.empty() && frames <= 0)) return 0;
 
-    rt_context* ctx = nullptr;
-    int rc = rt_create(device, &ctx);
-    if (rc) return die(ctx, rc, "rt_create");
+    if (gpus < 1) gpus = 1;
+    const int ndev = rt_device_count() > 0 ? rt_device_count() : 1;
+    std::vector<rt_context*> ctxs(gpus, nullptr);
+    int rc = 0;
     rt_scene view = sd.view();
-    if ((rc = rt_set_scene(ctx, &view))) return die(ctx, rc, "rt_set_scene");
-    if ((rc = rt_set_max_bounces(ctx, max_bounces))) return die(ctx, rc, "rt_set_max_bounces");
-    if ((rc = rt_set_background(ctx, bg[0], bg[1], bg[2]))) return die(ctx, rc, "rt_set_background");
+    for (int g = 0; g < gpus; g++) {
+        if ((rc = rt_create((device + g) % ndev, &ctxs[g]))) return die(ctxs[g], rc, "rt_create");
+        if ((rc = rt_set_scene(ctxs[g], &view))) return die(ctxs[g], rc, "rt_set_scene");
+        if ((rc = rt_set_max_bounces(ctxs[g], max_bounces))) return die(ctxs[g], rc, "rt_set_max_bounces");
+        if ((rc = rt_set_background(ctxs[g], bg[0], bg[1], bg[2]))) return die(ctxs[g], rc, "rt_set_background");
+    }
+    rt_context* ctx = ctxs[0];
     std::vector<uint8_t> rgba((size_t)width * height * 4);
     using clk = std::chrono::steady_clock;
     double delta = 0.0;
@@ -166,15 +173,20 @@ int main(int argc, char** argv) {
     for (int done = 0; done < frames;) {  // Main.cu:471-496
         const int n = std::min(per_call, frames - done);
         auto t0 = clk::now();
-        if ((rc = rt_render(ctx, width, height, n, rgba.data()))) return die(ctx, rc, "rt_render");
+        rc = gpus == 1 ? rt_render(ctx, width, height, n, rgba.data())
+                       : rt_render_multi(ctxs.data(), gpus, width, height, n, rgba.data());
+        if (rc) return die(ctx, rc, "rt_render");
         done += n;
         const double frame_s = std::chrono::duration<double>(clk::now() - t0).count();
         bool quit = false;
         if (!steps.empty()) {  // controls(window, camera, deltaTime, accumulatedFrames)
             const unsigned keys = steps[step].keys;
             if (--step_left == 0 && step + 1 < steps.size()) step_left = steps[++step].frames;
-            const int flags = rt_controls(ctx, keys, (float)(fixed_dt >= 0 ? fixed_dt : frame_s));
-            if (flags < 0) return die(ctx, flags, "rt_controls");
+            int flags = 0;
+            for (int g = 0; g < gpus; g++) {  // every context keeps the same camera / frame counter
+                flags = rt_controls(ctxs[g], keys, (float)(fixed_dt >= 0 ? fixed_dt : frame_s));
+                if (flags < 0) return die(ctxs[g], flags, "rt_controls");
+            }
             quit = flags & RT_CONTROLS_QUIT;
         }
         delta += frame_s;
@@ -200,6 +212,6 @@ int main(int argc, char** argv) {
     if (!steps.empty() && rt_get_camera(ctx, &cam) == RT_OK)
         std::printf("camera %.9g %.9g %.9g %.9g %.9g\n", cam.position.x, cam.position.y, cam.position.z,
                     cam.angle[0], cam.angle[1]);
-    rt_destroy(ctx);
+    for (rt_context* c : ctxs) rt_destroy(c);
     return 0;
 }

@@ -357,6 +357,13 @@ def test_cli_progressive_loop_with_controls(bwrt_lib, oracle, tmp_path):
     img = np.asarray(Image.open(png).convert("RGBA"))[::-1]
     assert np.array_equal(img, st.rgba)
     assert "camera" in r.stdout and "Samples: 4" in r.stdout
+    # the same loop across 3 contexts (rt_render_multi; one device here)
+    png3 = tmp_path / "out3.png"
+    r = subprocess.run([cli, "--scene", "07", "--width", "160", "--height", "90", "--frames", "6", "--gpus", "3",
+                        "--keys", "*1,W+LEFT*1,*9", "--dt", "0.05", "--out", str(png3)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(np.asarray(Image.open(png3).convert("RGBA"))[::-1], st.rgba)
 
 
 def test_repeated_renders_are_identical(gpu, oracle):
