@@ -106,6 +106,7 @@ int main(int argc, char** argv) {
                 return 2;
             }
         } else if (!std::strcmp(argv[i], "--device")) device = std::atoi(next());
+        else if (!std::strcmp(argv[i], "--gpus")) gpus = std::atoi(next());
         else if (!std::strcmp(argv[i], "--keys")) keys_spec = next();
         else if (!std::strcmp(argv[i], "--dt")) fixed_dt = std::atof(next());
         else if (!std::strcmp(argv[i], "--out")) out = next();
