@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true",
                     help="rank 0 re-renders the whole frame on its GPU alone and checks the gathered image")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: gather each frame before the next render starts (no frame pipelining)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
     return ap.parse_args()
@@ -125,17 +127,32 @@ def main():
     my_rows = lib.rt_shard_rows(H, plan.row_offset, plan.row_stride)
     assert my_rows == plan.rows
     r.init_rand(W, H, plan.row_offset, plan.row_stride)
-    local_img = torch.zeros(rows_per * W, dtype=torch.int32, device=dev)
+    # N > 1: frames are pipelined — frame k's gather + de-interleave run on a
+    # second stream while frame k+1 renders (double-buffered row blocks);
+    # the timed region still covers every render and every gather
+    overlap = world > 1 and not args.no_overlap
+    nbuf = 2 if overlap else 1
+    local_imgs = [torch.zeros(rows_per * W, dtype=torch.int32, device=dev) for _ in range(nbuf)]
     full_img = torch.empty(H * W, dtype=torch.int32, device=dev) if rank == 0 else None
-    gathered = torch.empty((world, rows_per * W), dtype=torch.int32, device=dev) if world > 1 else None
+    gathered = ([torch.empty((world, rows_per * W), dtype=torch.int32, device=dev) for _ in range(nbuf)]
+                if world > 1 else None)
     # a dedicated (non-null) stream: the kernel, its timing events and the
     # RCCL gather are all ordered on it (NULL would mean the context's own
     # stream in the C ABI)
     stream = torch.cuda.Stream(dev)
+    comm = torch.cuda.Stream(dev) if overlap else stream
     torch.cuda.set_stream(stream)
+    ev_rendered = [torch.cuda.Event() for _ in range(nbuf)]
+    ev_sent = [torch.cuda.Event() for _ in range(nbuf)]  # block b's last gather has read it
     params = r.params(W, H, SPP, MB, first_frame=1, row_offset=plan.row_offset, row_stride=plan.row_stride)
+    counter = [0]
 
     def step(ev=None):
+        b = counter[0] % nbuf
+        counter[0] += 1
+        local_img = local_imgs[b]
+        if overlap:
+            stream.wait_event(ev_sent[b])  # no-op until the event is first recorded
         if ev is not None:
             ev[0].record(stream)
         r.render_device(params, local_img.data_ptr() if world > 1 else full_img.data_ptr(),
@@ -143,10 +160,14 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            gather_rows(local_img, plan, out=gathered)
-            if rank == 0:
-                r.deinterleave_device(gathered.data_ptr(), full_img.data_ptr(), W, H, world, rows_per,
-                                      stream.cuda_stream)
+            ev_rendered[b].record(stream)
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev_rendered[b])
+                gather_rows(local_img, plan, out=gathered[b])
+                if rank == 0:
+                    r.deinterleave_device(gathered[b].data_ptr(), full_img.data_ptr(), W, H, world, rows_per,
+                                          comm.cuda_stream)
+                ev_sent[b].record(comm)
 
     for _ in range(args.warmup):
         step()
@@ -194,7 +215,8 @@ def main():
             "config": {"workload": f"07_specular_BRDF {W}x{H} {SPP}spp {MB}-bounce (BASELINE configs[2])"
                        if args.config == "c3" else f"{args.config}: scene {scene_key} {W}x{H} {SPP}spp {MB}-bounce",
                        "scene": scene_key, "width": W, "height": H, "spp": SPP, "max_bounces": MB,
-                       "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} all_gather" if world > 1 else "")},
+                       "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} all_gather" if world > 1 else "")
+                       + (" (frames pipelined: gather of frame k overlaps render of k+1)" if overlap else "")},
             "ms_per_frame": round(ms_step, 4),
             "kernel_ms_avg": round(kern_avg_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -22,7 +22,8 @@
 #include "../../include/rt_abi.h"
 #include "rt_layout.h"
 
-hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, hipStream_t stream);
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
+                            hipStream_t stream);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
                                hipStream_t stream);
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
@@ -91,6 +92,7 @@ struct rt_context {
     DevBuf rng, accum, rgba;
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
     size_t host_rgba_bytes = 0;
+    int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
     int tile_w = 16;             // BWRT_TILE: wave tile width (16 x 4 pixel waves; 0 = linear order)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
@@ -476,6 +478,7 @@ int rt_create(int device, rt_context** out) {
         c->num_cus = prop.multiProcessorCount;
     if (const char* gm = std::getenv("BWRT_GRID_MULT")) c->grid_mult = std::atoi(gm);
     if (const char* kk = std::getenv("BWRT_KERNEL")) c->simple = std::strcmp(kk, "simple") == 0;
+    if (const char* bk = std::getenv("BWRT_BLOCK")) c->block = std::atoi(bk);
     if (const char* tw = std::getenv("BWRT_TILE")) {
         const int t = std::atoi(tw);
         if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
@@ -876,7 +879,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     }
     K.tile_w = c->tile_w;
     HIP_TRY(c, hipEventRecord(c->ev0, s));
-    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, s);
+    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, s);
     if (stamps) {
         unsigned long long h[NST] = {0};
         (void)hipMemcpyAsync(h, stamps, sizeof h, hipMemcpyDeviceToHost, s);

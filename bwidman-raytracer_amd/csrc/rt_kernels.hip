@@ -1562,7 +1562,8 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 // sorted task-queue kernel unless `simple` (one pixel per lane: its grid
 // always covers every item); for the simple kernel grid_mult > 0 caps the
 // grid at grid_mult x resident workgroups per CU (persistent lanes).
-hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, hipStream_t stream) {
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
+                            hipStream_t stream) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = !K.bvh_nodes && (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
     const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 49152;
@@ -1575,6 +1576,14 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
 #define RT_SORTED_BLOCK 256
 #endif
     if (small_block) return launch_block<64, true>(K, hit_lds, lds, grid_mult, num_cus, stream);
+    if (block_req == 64 || block_req == 128 || block_req == 256) {  // explicit (BWRT_BLOCK)
+        const size_t lds_r = rt_render_lds_bytes(K, block_req, hit_lds, true);
+        if (lds_r <= 65536) {
+            if (block_req == 64) return launch_block<64, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
+            if (block_req == 128) return launch_block<128, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
+            return launch_block<256, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
+        }
+    }
     const size_t lds_s = rt_render_lds_bytes(K, RT_SORTED_BLOCK, hit_lds, true);
     // deep paths (large max_bounces) make the LDS record stack big: take
     // 128-lane groups when they keep more waves resident per CU (LDS 160 KB,
@@ -1583,8 +1592,15 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
         const long by_lds = (long)(160 * 1024 / (lds_bytes ? lds_bytes : 1)) * (block / 64);
         return by_lds < 4L * RT_WAVES_PER_EU ? by_lds : 4L * RT_WAVES_PER_EU;
     };
+    // small frames / shards (one rank of an 8-GPU frame): fewer than 4
+    // full-size groups per CU leave CUs with unequal shares of the critical
+    // path (every group is resident at once); 128-lane groups spread it
+    // (measured on c3 row shards of 1/8: 0.249 vs 0.264 ms; 1/4: 0.312 vs 0.291)
+    const long items = (long)K.rows * K.width;
+    const bool few_groups = items < (long)num_cus * 4 * RT_SORTED_BLOCK;
     if (RT_SORTED_BLOCK > 128 &&
-        waves_per_cu(rt_render_lds_bytes(K, 128, hit_lds, true), 128) > waves_per_cu(lds_s, RT_SORTED_BLOCK)) {
+        (few_groups ||
+         waves_per_cu(rt_render_lds_bytes(K, 128, hit_lds, true), 128) > waves_per_cu(lds_s, RT_SORTED_BLOCK))) {
         const size_t lds_128 = rt_render_lds_bytes(K, 128, hit_lds, true);
         return launch_block<128, true>(K, hit_lds, lds_128, grid_mult, num_cus, stream);
     }

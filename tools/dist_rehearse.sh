@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out
+for n in 2 3; do
+  for ov in "" "--no-overlap"; do
+    BWRT_DIST_BACKEND=gloo timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus $n --steps 10 --warmup 3 --verify $ov > gpurun_out/dist_$n$ov.log 2>&1 || { echo "FAIL $n $ov"; tail -20 gpurun_out/dist_$n$ov.log; exit 1; }
+    echo "n=$n $ov: $(grep -o '"ms_per_step[^,]*' gpurun_out/dist_$n$ov.log) $(grep verify gpurun_out/dist_$n$ov.log)"
+  done
+done
+timeout -k 10 100 python -u tools/shard_sweep.py --blocks 0 --strides 1,2,4,8 2>&1 | grep -v amdgpu.ids
+timeout -k 10 100 python bench.py --no-cpu-baseline 2>&1 | tail -1
