@@ -90,7 +90,6 @@ struct rt_context {
     // shard state
     int width = 0, height = 0, row_offset = 0, row_stride = 1, rows = 0;
     DevBuf rng, accum, rgba;
-    DevBuf pool;  // global pixel-pool counter (RT_POOL builds)
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
     size_t host_rgba_bytes = 0;
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
@@ -497,7 +496,6 @@ void rt_destroy(rt_context* c) {
     free_buf(c->rng);
     free_buf(c->accum);
     free_buf(c->rgba);
-    free_buf(c->pool);
     if (c->host_rgba) (void)hipHostFree(c->host_rgba);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -879,41 +877,9 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
             (void)hipMemsetAsync(stamps, 0, NST * sizeof(unsigned long long), s);
         K.stamps = stamps;
     }
-    const char* gtimes = std::getenv("BWRT_GTIMES");  // diagnostic builds (-DRT_GTIMES): group times file
-    const size_t NGT = (size_t)1 << 22;
-    if (gtimes && !stamps) {
-        if (hipMalloc(&stamps, NGT * sizeof(unsigned long long)) == hipSuccess)
-            (void)hipMemsetAsync(stamps, 0, NGT * sizeof(unsigned long long), s);
-        K.stamps = stamps;
-    }
     K.tile_w = c->tile_w;
-#ifdef RT_POOL
-    {
-        long nitems = (long)K.rows * K.width;  // rt_kernels.hip items_of()
-        if (K.tile_w > 0) {
-            const long tx = (K.width + K.tile_w - 1) / K.tile_w, ty = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
-            nitems = tx * ty * 64;
-        }
-        K.pool_chunks = (int)((nitems + 63) / 64);
-        int rc = ensure_buf(c, c->pool, sizeof(int));
-        if (rc) return rc;
-        K.pool = (int*)c->pool.p;
-        HIP_TRY(c, hipMemsetAsync(c->pool.p, 0, sizeof(int), s));
-    }
-#endif
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, s);
-    if (gtimes && stamps) {
-        std::vector<unsigned long long> h(NGT);
-        (void)hipMemcpyAsync(h.data(), stamps, NGT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
-        (void)hipStreamSynchronize(s);
-        if (FILE* f = std::fopen(gtimes, "wb")) {
-            std::fwrite(h.data(), sizeof(unsigned long long), NGT, f);
-            std::fclose(f);
-        }
-        (void)hipFree(stamps);
-        stamps = nullptr;
-    }
     if (stamps) {
         unsigned long long h[NST] = {0};
         (void)hipMemcpyAsync(h, stamps, sizeof h, hipMemcpyDeviceToHost, s);

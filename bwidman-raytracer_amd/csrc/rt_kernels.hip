@@ -31,9 +31,6 @@
 //    per-ray math, not a contraction).
 #include <hip/hip_runtime.h>
 
-#include <cstdio>
-#include <cstdlib>
-
 #include "rt_layout.h"
 
 namespace {
@@ -803,88 +800,6 @@ __device__ __forceinline__ void load_item(const rt_kparams& K, long npix, long n
     s.w = w;
 }
 
-#ifdef RT_POOL
-// Launch constants the pool's switch / claim code needs, staged in LDS at
-// kernel start: read (rarely) through LDS inside the loop, so they do not
-// keep ~25 SGPRs live across it (the loop is at the SGPR limit already).
-struct PoolLds {
-    float rot[9];
-    float screen_z;
-    int width, half_w, half_h, row_offset, row_stride;
-    int tile_w, tiles_x, pool_chunks;
-    long npix, nitems;
-    unsigned* rng;
-    float* accum;
-    int* pool;
-    unsigned first_frame;
-    int samples;
-};
-
-__device__ __forceinline__ long pool_item_to_pixel(const PoolLds& P, long w) {  // item_to_pixel()
-    if (w >= P.nitems) return P.npix;
-    if (P.tile_w <= 0) return w;
-    const int tw = P.tile_w, th = 64 / P.tile_w;
-    const long wave = w >> 6;
-    const int l = (int)(w & 63);
-    const long x = (wave % P.tiles_x) * tw + (l % tw);
-    const long j = (wave / P.tiles_x) * th + (l / tw);
-    const long rows = P.npix / P.width;
-    if (x >= P.width || j >= rows) return P.npix;
-    return j * P.width + x;
-}
-
-// switch a lane to pixel p (RNG state already fetched into rs): Main.cu:287-290
-// camera direction, frameSum carried over unless the launch starts at frame 1
-__device__ __forceinline__ void install_pixel(const PoolLds& P, long p, const Xorwow& rs, PixelState& s) {
-    s.p = p;
-    s.valid = true;
-    s.rs = rs;
-    s.frame = P.first_frame;
-    s.passes_left = P.samples;
-    s.ax = s.ay = s.az = 0.0f;
-    if (P.first_frame != 1u) {
-        s.ax = P.accum[0 * P.npix + p];
-        s.ay = P.accum[1 * P.npix + p];
-        s.az = P.accum[2 * P.npix + p];
-    }
-    const int j = (int)(p / P.width);
-    const int x = (int)(p - (long)j * P.width);
-    const int y = P.row_offset + j * P.row_stride;
-    const f3 pix = mk((float)(x - P.half_w), (float)(y - P.half_h), P.screen_z);
-    const f3 pr = mk(P.rot[0] * pix.x + P.rot[1] * pix.y + P.rot[2] * pix.z,
-                     P.rot[3] * pix.x + P.rot[4] * pix.y + P.rot[5] * pix.z,
-                     P.rot[6] * pix.x + P.rot[7] * pix.y + P.rot[8] * pix.z);
-    s.d0 = normalize3(pr);
-}
-
-__device__ __forceinline__ void store_state_lds(const PoolLds& P, const PixelState& s) {
-    const long p = s.p, n = P.npix;
-    P.rng[0 * n + p] = s.rs.d;
-    P.rng[1 * n + p] = s.rs.v0;
-    P.rng[2 * n + p] = s.rs.v1;
-    P.rng[3 * n + p] = s.rs.v2;
-    P.rng[4 * n + p] = s.rs.v3;
-    P.rng[5 * n + p] = s.rs.v4;
-    P.accum[0 * n + p] = s.ax;
-    P.accum[1 * n + p] = s.ay;
-    P.accum[2 * n + p] = s.az;
-}
-
-// RNG state + frameSum of a finished pixel (the image comes from the tone-map pass)
-__device__ __forceinline__ void store_state(const rt_kparams& K, long npix, const PixelState& s) {
-    const long p = s.p;
-    K.rng[0 * npix + p] = s.rs.d;
-    K.rng[1 * npix + p] = s.rs.v0;
-    K.rng[2 * npix + p] = s.rs.v1;
-    K.rng[3 * npix + p] = s.rs.v2;
-    K.rng[4 * npix + p] = s.rs.v3;
-    K.rng[5 * npix + p] = s.rs.v4;
-    K.accum[0 * npix + p] = s.ax;
-    K.accum[1 * npix + p] = s.ay;
-    K.accum[2 * npix + p] = s.az;
-}
-#endif
-
 __device__ __forceinline__ void store_pixel(const rt_kparams& K, long npix, const PixelState& s) {
     const long p = s.p;
     K.rng[0 * npix + p] = s.rs.d;
@@ -973,13 +888,6 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 // previous one ends.  A wave ends when all its lanes ran out of pixels.
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 1
-#endif
-// ints after the slots: 3 queue counters x 2 parities (+ pool state and ring)
-#ifdef RT_POOL
-#define RT_POOL_RING 8
-#define RT_COUNTER_INTS (20 + (int)(sizeof(PoolLds) / 4))
-#else
-#define RT_COUNTER_INTS 6
 #endif
 // s_setprio of the wave that runs SPEC tasks during the execute step (the
 // longest wave there; measured 0.882 -> 0.876 ms); 0 disables
@@ -1163,16 +1071,6 @@ rt_render_kernel(rt_kparams K) {
 #undef STAMP
 }
 
-#ifdef RT_POOL
-// frameSum / n -> RGBA8 for every pixel (Main.cu:305-312), after the pooled render
-static __global__ void __launch_bounds__(256) rt_tonemap_kernel(const float* __restrict__ accum, unsigned* __restrict__ rgba,
-                                                         long npix, unsigned n) {
-    const long p = (long)blockIdx.x * 256 + threadIdx.x;
-    if (p >= npix) return;
-    rgba[p] = tone_map(accum[p], accum[npix + p], accum[2 * npix + p], n);
-}
-#endif
-
 #ifndef RT_TU_BVH  // defined once, in the main translation unit
 // initializeRand (Main.cu:369-380): curand_init(y*W + x, 0, 0)
 __global__ void __launch_bounds__(256) rt_init_rand_kernel(unsigned* rng, int width, int rows,
@@ -1197,7 +1095,6 @@ __global__ void __launch_bounds__(256) rt_init_rand_kernel(unsigned* rng, int wi
 }
 
 // Multi-GPU gather epilogue: block r of `gathered` holds rows r, r+G, ...
-
 __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __restrict__ gathered,
                                                               unsigned* __restrict__ image, int width,
                                                               int height, int shards, int rows_per_shard) {
@@ -1267,49 +1164,10 @@ rt_render_sorted_kernel(rt_kparams K) {
 #else
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
 #endif
-    // counters[0..5]: queue front / back / pool claims, 2 parities;
-    // RT_POOL: [6] head (claimed items), [7] avail (items in the ring),
-    // [8] global pool exhausted, [9..9+RT_POOL_RING) ring of chunk ids
+    // counters[0..3]: queue fronts/backs (2 parities)
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
-    if (tid < 6) counters[tid] = 0;
-#ifdef RT_POOL
-    int* pst = counters + 6;
-    int* ring = counters + 9;
-    PoolLds* pl = reinterpret_cast<PoolLds*>(counters + 20);  // 16-byte aligned
-    if (tid == 0) {
-        for (int k = 0; k < 9; k++) pl->rot[k] = K.rot[k];
-        pl->screen_z = K.screen_z;
-        pl->width = K.width;
-        pl->half_w = K.width / 2;
-        pl->half_h = K.height / 2;
-        pl->row_offset = K.row_offset;
-        pl->row_stride = K.row_stride;
-        pl->tile_w = K.tile_w;
-        pl->tiles_x = K.tile_w > 0 ? (K.width + K.tile_w - 1) / K.tile_w : 0;
-        pl->pool_chunks = K.pool_chunks;
-        pl->npix = npix;
-        pl->nitems = nitems;
-        pl->rng = K.rng;
-        pl->accum = K.accum;
-        pl->pool = K.pool;
-        pl->first_frame = K.first_frame;
-        pl->samples = K.samples;
-    }
-    if (tid == 0) {  // first BLOCK/64 chunks: one wave tile per wave, as without the pool
-        const int want_ch = BLOCK / 64;
-        const int b = atomicAdd(K.pool, want_ch);
-        const int got = max(0, min(want_ch, K.pool_chunks - b));
-        for (int k = 0; k < got; k++) ring[k] = b + k;
-        pst[0] = 64 * got;
-        pst[1] = 64 * got;
-        pst[2] = b + want_ch >= K.pool_chunks;
-    }
-#endif
-#ifdef RT_GTIMES
-    // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g], [2g+1]
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
+    if (tid < 4) counters[tid] = 0;
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
 // task results {r.xyz, kspec, rng[6]}: a separate mailbox (RT_MAILBOX), or
@@ -1321,17 +1179,7 @@ rt_render_sorted_kernel(rt_kparams K) {
 #endif
 
     PixelState px;
-#ifdef RT_POOL
-    load_item(K, npix, nitems, tid < pst[1] ? (long)ring[tid >> 6] * 64 + (tid & 63) : nitems, px);
-    // want: ask the pool for the next pixel (from the start of the last
-    // frame, so its RNG state has landed by the time the lane switches)
-    bool want = !px.valid || px.passes_left == 1;
-    long nxt = -1;  // claimed next pixel
-    Xorwow nrs;
-    nrs.d = nrs.v0 = nrs.v1 = nrs.v2 = nrs.v3 = nrs.v4 = 0u;
-#else
     load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
-#endif
     int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -1358,9 +1206,6 @@ rt_render_sorted_kernel(rt_kparams K) {
         px.az = px.az + lz;
         px.frame++;
         px.passes_left--;
-#ifdef RT_POOL
-        if (px.passes_left == 1) want = true;
-#endif
         // one pixel per lane (the grid covers every work item): a finished
         // pixel is stored after the loop, by the whole wave at once, and the
         // camera set-up constants are not live inside the loop
@@ -1396,15 +1241,6 @@ rt_render_sorted_kernel(rt_kparams K) {
     } while (0)
 #endif
     while (true) {
-#ifdef RT_POOL
-        if (px.passes_left == 0 && nxt >= 0) {  // pixel done: write it back, take the claimed one
-            if (px.valid && px.frame != pl->first_frame) store_state_lds(*pl, px);
-            install_pixel(*pl, nxt, nrs, px);
-            nxt = -1;
-            mode = M_REGEN;
-            want = px.passes_left == 1;
-        }
-#endif
         const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
         STAMP(7);
 #ifndef RT_MAILBOX
@@ -1415,49 +1251,15 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(0);
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
-        int* cnt = counters + 3 * parity;
+        int* cnt = counters + 2 * parity;
         const bool front = task == T_REGEN || task == T_DIFF;
         const unsigned long long mf = __ballot(front);
         const unsigned long long mbk = __ballot(task == T_SPEC);
         int base_f = 0, base_b = 0;
-#ifdef RT_POOL
-        // pool claims: items head + k in claim order (head / avail / ring are
-        // only written by thread 0 outside this phase)
-        const int p_head = pst[0], p_avail = pst[1];
-        const bool attempt = want && (p_head < p_avail || !pst[2]);
-        const unsigned long long mcl = __ballot(attempt);
-        int base_c = 0;
-        if (lane == 0) {
-            if (mf) base_f = atomicAdd(&cnt[0], __popcll(mf));
-            if (mbk) base_b = atomicAdd(&cnt[1], __popcll(mbk));
-            if (mcl) base_c = atomicAdd(&cnt[2], __popcll(mcl));
-        }
-        base_c = __builtin_amdgcn_readfirstlane(base_c);
-        if (attempt) {
-            const int c = p_head + base_c + lanes_below(mcl);
-            if (c < p_avail) {
-                const PoolLds& P = *pl;
-                const long it = (long)ring[(c >> 6) & (RT_POOL_RING - 1)] * 64 + (c & 63);
-                const long pn = pool_item_to_pixel(P, it);
-                if (pn < P.npix) {  // (padding items of partial tiles are skipped)
-                    const long n = P.npix;
-                    nxt = pn;
-                    want = false;
-                    nrs.d = P.rng[0 * n + pn];
-                    nrs.v0 = P.rng[1 * n + pn];
-                    nrs.v1 = P.rng[2 * n + pn];
-                    nrs.v2 = P.rng[3 * n + pn];
-                    nrs.v3 = P.rng[4 * n + pn];
-                    nrs.v4 = P.rng[5 * n + pn];
-                }
-            }
-        }
-#else
         if (lane == 0) {
             if (mf) base_f = atomicAdd(&cnt[0], __popcll(mf));
             if (mbk) base_b = atomicAdd(&cnt[1], __popcll(mbk));
         }
-#endif
         base_f = __builtin_amdgcn_readfirstlane(base_f);
         base_b = __builtin_amdgcn_readfirstlane(base_b);
         int slot = -1;
@@ -1485,28 +1287,14 @@ rt_render_sorted_kernel(rt_kparams K) {
         // no task anywhere in the workgroup: every lane is idle (rays are
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
-#ifdef RT_POOL
-        // claims keep the group alive: a lane that claimed while idle switches
-        // next round, one that found the ring empty retries after the refill
-        const int ncl = cnt[2];
-        if (nf + nb + ncl == 0) break;
-        int fetched = -1;
-        if (tid == 0) {
-            const int hnew = min(p_head + ncl, p_avail);
-            pst[0] = hnew;
-            if (!pst[2] && p_avail - hnew < BLOCK) fetched = atomicAdd(pl->pool, 1);  // used at the round end
-        }
-#else
         if (nf + nb == 0) break;
-#endif
 #ifdef RT_MAILBOX
         // next round's counters were last read before the previous round's
         // second barrier; the barrier after the execute step orders this
         // reset before any wave posts next round's tasks
         if (tid == 0) {
-            counters[3 * (parity ^ 1)] = 0;
-            counters[3 * (parity ^ 1) + 1] = 0;
-            counters[3 * (parity ^ 1) + 2] = 0;
+            counters[2 * (parity ^ 1)] = 0;
+            counters[2 * (parity ^ 1) + 1] = 0;
         }
 #endif
 
@@ -1591,9 +1379,8 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(4);
 #ifndef RT_MAILBOX
         if (tid == 0) {
-            counters[3 * (parity ^ 1)] = 0;
-            counters[3 * (parity ^ 1) + 1] = 0;
-            counters[3 * (parity ^ 1) + 2] = 0;
+            counters[2 * (parity ^ 1)] = 0;
+            counters[2 * (parity ^ 1) + 1] = 0;
         }
 #endif
         parity ^= 1;
@@ -1673,27 +1460,9 @@ rt_render_sorted_kernel(rt_kparams K) {
             ended = false;
             finish_path(slot);
         }
-#ifdef RT_POOL
-        if (tid == 0 && fetched >= 0) {  // refill (before the next round's first barrier)
-            if (fetched < pl->pool_chunks) {
-                ring[(p_avail >> 6) & (RT_POOL_RING - 1)] = fetched;
-                pst[1] = p_avail + 64;
-            } else {
-                pst[2] = 1;
-            }
-        }
-#endif
         STAMP(6);
     }
-#ifdef RT_POOL
-    if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_state(K, npix, px);
-#else
     if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
-#endif
-#ifdef RT_GTIMES
-    __syncthreads();
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
 #ifdef RT_STAMPS
     if ((threadIdx.x & 63) == 0 && K.stamps) {
         for (int k = 0; k < 8; k++) atomicAdd(&K.stamps[k], st_acc[k]);
@@ -1733,35 +1502,12 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
             if (grid > cap) grid = cap;
         }
     }
-#ifdef RT_POOL
-    if (SORTED) {  // persistent: at most the resident workgroups, pixels from the global pool
-        // resident groups per CU: 160 KB of LDS (gfx950) and RT_WAVES_PER_EU
-        // waves per SIMD (the launch bound caps the VGPRs accordingly)
-        const long by_lds = (long)(160 * 1024) / (long)(lds ? lds : 1);
-        const long by_waves = 4L * RT_WAVES_PER_EU / (BLOCK / 64);
-        const long per_cu = by_lds < by_waves ? by_lds : by_waves;
-        const long need = ((long)K.pool_chunks + BLOCK / 64 - 1) / (BLOCK / 64);
-        grid = min(need, (per_cu > 0 ? per_cu : 1) * num_cus);
-        if (std::getenv("BWRT_DEBUG")) {
-            int api = 0;
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH>(), BLOCK, lds);
-            fprintf(stderr, "pool grid %ld (per_cu %ld, occupancy api %d, lds %zu, cus %d)\n", grid, per_cu, api, lds, num_cus);
-        }
-    }
-#endif
     if (grid < 1) grid = 1;
     if (SORTED)
         hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream,
                            K);
     else
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
-#ifdef RT_POOL
-    if (SORTED && K.rgba) {  // Main.cu:305-312 for every pixel of the shard
-        const long npix = (long)K.rows * K.width;
-        hipLaunchKernelGGL(rt_tonemap_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, stream,
-                           (const float*)K.accum, K.rgba, npix, K.first_frame + (unsigned)K.samples - 1u);
-    }
-#endif
     return hipGetLastError();
 }
 
@@ -1804,9 +1550,9 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
     size_t b = hit + (size_t)3 * (K.max_bounces + (sorted ? 0 : 1)) * block * sizeof(float);
 #ifdef RT_MAILBOX
-    if (sorted) b += (size_t)23 * block * sizeof(float) + RT_COUNTER_INTS * sizeof(int);
+    if (sorted) b += (size_t)23 * block * sizeof(float) + 4 * sizeof(int);
 #else
-    if (sorted) b += (size_t)13 * block * sizeof(float) + RT_COUNTER_INTS * sizeof(int);
+    if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
 #endif
     return b;
 }

@@ -80,12 +80,6 @@ struct rt_kparams {
     // conservative polygon culling (see polygon_test): only rays whose origin
     // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
     float cull_omax;
-    // global pixel pool (sorted kernel built with RT_POOL): chunks of 64
-    // work items (one wave tile) handed out by an atomic counter to
-    // persistent workgroups; the RGBA image is then written by a separate
-    // tone-map pass
-    int* pool;
-    int pool_chunks;
 };
 
 // Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,

@@ -22,7 +22,6 @@ def main():
     ap.add_argument("--blocks", default="0,64,128,256")
     ap.add_argument("--tiles", default="16")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--spp", default="", help="comma list overriding the config's spp")
     a = ap.parse_args()
     key, W, H, SPP, MB, _ = scenes.CONFIGS[a.config]
     lib = abi.load()
@@ -34,10 +33,10 @@ def main():
             os.environ["BWRT_TILE"] = str(tile)
             r = Renderer(0, lib=lib)
             r.set_scene(scenes.SCENES[key]())
-            for g, spp in [(int(s), int(q)) for s in a.strides.split(",") for q in (a.spp or str(SPP)).split(",")]:
+            for g in [int(s) for s in a.strides.split(",")]:
                 rows = -(-H // g)
                 img = torch.empty(rows * W, dtype=torch.int32, device=dev)
-                p = r.params(W, H, spp, MB, first_frame=1, row_offset=0, row_stride=g)
+                p = r.params(W, H, SPP, MB, first_frame=1, row_offset=0, row_stride=g)
                 r.init_rand(W, H, 0, g)
                 for _ in range(3):
                     r.render_device(p, img.data_ptr(), stream.cuda_stream)
@@ -49,7 +48,7 @@ def main():
                     e1.record(stream)
                 torch.cuda.synchronize()
                 ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)
-                print(f"{a.config} spp {spp} tile {tile:2d} block {blk:3d} stride {g}: median {ms[len(ms)//2]:.4f} ms "
+                print(f"{a.config} tile {tile:2d} block {blk:3d} stride {g}: median {ms[len(ms)//2]:.4f} ms "
                       f"min {ms[0]:.4f}  (x{g} = {ms[len(ms)//2]*g:.4f})", flush=True)
             r.close()
 
