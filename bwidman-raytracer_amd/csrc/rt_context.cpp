@@ -877,9 +877,27 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
             (void)hipMemsetAsync(stamps, 0, NST * sizeof(unsigned long long), s);
         K.stamps = stamps;
     }
+    const char* gtimes = std::getenv("BWRT_GTIMES");  // diagnostic builds (-DRT_GTIMES): group times file
+    const size_t NGT = (size_t)1 << 22;
+    if (gtimes && !stamps) {
+        if (hipMalloc(&stamps, NGT * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemsetAsync(stamps, 0, NGT * sizeof(unsigned long long), s);
+        K.stamps = stamps;
+    }
     K.tile_w = c->tile_w;
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, s);
+    if (gtimes && stamps) {
+        std::vector<unsigned long long> h(NGT);
+        (void)hipMemcpyAsync(h.data(), stamps, NGT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        if (FILE* f = std::fopen(gtimes, "wb")) {
+            std::fwrite(h.data(), sizeof(unsigned long long), NGT, f);
+            std::fclose(f);
+        }
+        (void)hipFree(stamps);
+        stamps = nullptr;
+    }
     if (stamps) {
         unsigned long long h[NST] = {0};
         (void)hipMemcpyAsync(h, stamps, sizeof h, hipMemcpyDeviceToHost, s);

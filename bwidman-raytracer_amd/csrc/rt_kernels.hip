@@ -1168,6 +1168,10 @@ rt_render_sorted_kernel(rt_kparams K) {
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
     if (tid < 4) counters[tid] = 0;
+#ifdef RT_GTIMES
+    // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g], [2g+1]
+    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
 // task results {r.xyz, kspec, rng[6]}: a separate mailbox (RT_MAILBOX), or
@@ -1463,6 +1467,10 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(6);
     }
     if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
+#ifdef RT_GTIMES
+    __syncthreads();
+    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef RT_STAMPS
     if ((threadIdx.x & 63) == 0 && K.stamps) {
         for (int k = 0; k < 8; k++) atomicAdd(&K.stamps[k], st_acc[k]);
