@@ -2,7 +2,7 @@ import os, sys
 sys.path[:0] = ["bwidman-raytracer_amd"]
 import torch
 from bwrt import Renderer, abi, scenes
-key, W, H, SPP, MB, _ = scenes.CONFIGS["c3"]
+key, W, H, SPP, MB, _ = scenes.CONFIGS[os.environ.get("CFG", "c3")]
 lib = abi.load()
 r = Renderer(0, lib=lib); r.set_scene(scenes.SCENES[key]())
 for g in [int(x) for x in sys.argv[1:]]:
