@@ -22,6 +22,8 @@
 #include "../../include/rt_abi.h"
 #include "rt_layout.h"
 
+size_t rt_render_rec_floats(const rt_kparams& K);
+bool rt_render_wants_global_records(const rt_kparams& K);
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
                             hipStream_t stream);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
@@ -90,6 +92,8 @@ struct rt_context {
     // shard state
     int width = 0, height = 0, row_offset = 0, row_stride = 1, rows = 0;
     DevBuf rng, accum, rgba;
+    DevBuf rec;  // sorted kernel's record stack in global memory (deep paths)
+    int grec = -1;  // BWRT_GREC: 1 / 0 force global / LDS records; -1 = launch policy
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
     size_t host_rgba_bytes = 0;
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
@@ -483,6 +487,7 @@ int rt_create(int device, rt_context** out) {
         const int t = std::atoi(tw);
         if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
     }
+    if (const char* g = std::getenv("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
     *out = c;
     return RT_OK;
 }
@@ -496,6 +501,7 @@ void rt_destroy(rt_context* c) {
     free_buf(c->rng);
     free_buf(c->accum);
     free_buf(c->rgba);
+    free_buf(c->rec);
     if (c->host_rgba) (void)hipHostFree(c->host_rgba);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -885,6 +891,11 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.stamps = stamps;
     }
     K.tile_w = c->tile_w;
+    K.rec = nullptr;
+    if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {
+        const size_t floats = rt_render_rec_floats(K);
+        if (ensure_buf(c, c->rec, floats * sizeof(float)) == RT_OK) K.rec = (float*)c->rec.p;
+    }
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, s);
     if (gtimes && stamps) {

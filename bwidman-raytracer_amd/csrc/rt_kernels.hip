@@ -862,11 +862,11 @@ __device__ __forceinline__ void fold_level(int c0, float k, float c, const float
 }
 
 // Folds levels depth-1 .. 0 of the LDS record stack into L (in/out).
-template <int BLOCK>
-__device__ __forceinline__ void fold_records(const int* rec_code, const float* rec_k, const float* rec_c,
+// `rs`: distance between levels (BLOCK in LDS, the grid's lanes in global memory)
+__device__ __forceinline__ void fold_records(const int* rec_code, const float* rec_k, const float* rec_c, int rs,
                                              int depth, const float* hit_tab, float& lx, float& ly, float& lz) {
     for (int l = depth - 1; l >= 0; --l)
-        fold_level(rec_code[l * BLOCK], rec_k[l * BLOCK], rec_c[l * BLOCK], hit_tab, lx, ly, lz);
+        fold_level(rec_code[l * rs], rec_k[l * rs], rec_c[l * rs], hit_tab, lx, ly, lz);
 }
 
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
@@ -1133,7 +1133,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 //
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
-template <int BLOCK, bool HIT_LDS, bool BVH>
+template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
     enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
@@ -1153,10 +1153,14 @@ rt_render_sorted_kernel(rt_kparams K) {
     // the path in the round it is made, so it is folded straight from the
     // lane's own task slot (fields 4..6, free once the result is taken)
     const int levels = K.max_bounces;
-    int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
-    float* rec_k = rec_base + levels * BLOCK + tid;
-    float* rec_c = rec_base + 2 * levels * BLOCK + tid;
-    float* slots = rec_base + 3 * levels * BLOCK;
+    // record stack: LDS [field][level][lane], or (GREC) the same layout in
+    // global memory over the grid's lanes, which leaves LDS to the task slots
+    const int RS = GREC ? K.rec_stride : BLOCK;
+    float* rec_mem = GREC ? K.rec + (long)blockIdx.x * BLOCK : rec_base;
+    int* rec_code = reinterpret_cast<int*>(rec_mem) + tid;
+    float* rec_k = rec_mem + levels * RS + tid;
+    float* rec_c = rec_mem + 2 * levels * RS + tid;
+    float* slots = GREC ? rec_base : rec_base + 3 * levels * BLOCK;
 #ifdef RT_MAILBOX
     float* mbox = slots + 13 * BLOCK;  // task results: r.xyz, kspec, rng[6]
     int* counters = reinterpret_cast<int*>(mbox + 10 * BLOCK);
@@ -1198,8 +1202,7 @@ rt_render_sorted_kernel(rt_kparams K) {
         float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
         if (depth > K.max_bounces)  // deepest level, parked in the slot
             fold_level(__float_as_int(SLOT(6, slot)), SLOT(4, slot), SLOT(5, slot), hit_tab, lx, ly, lz);
-        fold_records<BLOCK>(rec_code, rec_k, rec_c, depth > K.max_bounces ? K.max_bounces : depth, hit_tab, lx, ly,
-                            lz);
+        fold_records(rec_code, rec_k, rec_c, RS, depth > K.max_bounces ? K.max_bounces : depth, hit_tab, lx, ly, lz);
         if (px.frame == 1u) {
             px.ax = 0.0f;
             px.ay = 0.0f;
@@ -1415,9 +1418,9 @@ rt_render_sorted_kernel(rt_kparams K) {
                 const float kspec = task == T_SPEC ? RES(3, slot) : 0.0f;
                 const float cosang = dot(r, hn);  // cosAngle, Main.cu:264
                 if (depth < K.max_bounces) {
-                    rec_code[depth * BLOCK] = code;
-                    rec_k[depth * BLOCK] = kspec;
-                    rec_c[depth * BLOCK] = cosang;
+                    rec_code[depth * RS] = code;
+                    rec_k[depth * RS] = kspec;
+                    rec_c[depth * RS] = cosang;
                     o = hP;
                     d = r;
                     has_ray = true;
@@ -1487,14 +1490,15 @@ rt_render_sorted_kernel(rt_kparams K) {
 
 // ---- launchers (host side) ------------------------------------------------
 namespace {
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH>
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC>
 void* kernel_ptr() {
-    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH>)
+    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC>)
                   : reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
 }
 
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH>
-hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC = false>
+hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
+    rt_kparams K = K0;
     long nitems = (long)K.rows * K.width;
     if (K.tile_w > 0) {
         const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
@@ -1503,7 +1507,7 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
     long grid = (nitems + BLOCK - 1) / BLOCK;  // streaming needs a resident grid only
     if (grid_mult > 0 && !SORTED) {  // persistent (simple kernel): grid_mult x resident groups per CU x CUs
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH>(), BLOCK, lds) ==
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC>(), BLOCK, lds) ==
                 hipSuccess &&
             per_cu > 0) {
             const long cap = (long)per_cu * num_cus * grid_mult;
@@ -1511,9 +1515,10 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
         }
     }
     if (grid < 1) grid = 1;
+    K.rec_stride = (int)(grid * BLOCK);
     if (SORTED)
-        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream,
-                           K);
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC>), dim3((unsigned)grid), dim3(BLOCK), lds,
+                           stream, K);
     else
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
     return hipGetLastError();
@@ -1527,14 +1532,18 @@ hipError_t launch_render(const rt_kparams& K, size_t lds, int grid_mult, int num
 // optimizer while the brute-force kernels are faster at -O1.
 hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
                                 hipStream_t s) {
+    const bool grec = sorted && K.rec;
     if (block == 64)
-        return sorted ? launch_render<64, false, true, true>(K, lds, grid_mult, num_cus, s)
-                      : launch_render<64, false, false, true>(K, lds, grid_mult, num_cus, s);
+        return grec ? launch_render<64, false, true, true, true>(K, lds, grid_mult, num_cus, s)
+                    : sorted ? launch_render<64, false, true, true>(K, lds, grid_mult, num_cus, s)
+                             : launch_render<64, false, false, true>(K, lds, grid_mult, num_cus, s);
     if (block == 128)
-        return sorted ? launch_render<128, false, true, true>(K, lds, grid_mult, num_cus, s)
-                      : launch_render<128, false, false, true>(K, lds, grid_mult, num_cus, s);
-    return sorted ? launch_render<256, false, true, true>(K, lds, grid_mult, num_cus, s)
-                  : launch_render<256, false, false, true>(K, lds, grid_mult, num_cus, s);
+        return grec ? launch_render<128, false, true, true, true>(K, lds, grid_mult, num_cus, s)
+                    : sorted ? launch_render<128, false, true, true>(K, lds, grid_mult, num_cus, s)
+                             : launch_render<128, false, false, true>(K, lds, grid_mult, num_cus, s);
+    return grec ? launch_render<256, false, true, true, true>(K, lds, grid_mult, num_cus, s)
+                : sorted ? launch_render<256, false, true, true>(K, lds, grid_mult, num_cus, s)
+                         : launch_render<256, false, false, true>(K, lds, grid_mult, num_cus, s);
 }
 #else
 hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
@@ -1545,10 +1554,43 @@ template <int BLOCK, bool SORTED>
 hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s) {
     if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
         return rt_launch_render_bvh(K, BLOCK, SORTED, lds, grid_mult, num_cus, s);
+    if (SORTED && K.rec)  // record stack in global memory
+        return hit_lds ? launch_render<BLOCK, true, SORTED, false, true>(K, lds, grid_mult, num_cus, s)
+                       : launch_render<BLOCK, false, SORTED, false, true>(K, lds, grid_mult, num_cus, s);
     return hit_lds ? launch_render<BLOCK, true, SORTED, false>(K, lds, grid_mult, num_cus, s)
                    : launch_render<BLOCK, false, SORTED, false>(K, lds, grid_mult, num_cus, s);
 }
 }  // namespace
+
+// Launch policy for the sorted kernel's record stack: global memory when the
+// LDS stack (3 dwords per level per lane) would hold the brute-force kernel
+// below RT_WAVES_PER_EU waves per SIMD, i.e. deep paths.  Measured: config
+// 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms; config 3 (maxBounces
+// 4, 6 waves with LDS records) 0.91 ms vs 0.95 in global memory; the BVH
+// kernel (VGPR-bound at 5 waves) 245 vs 255 ms, so it keeps LDS records.
+size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted);
+bool rt_render_wants_global_records(const rt_kparams& K) {
+    if (K.bvh_nodes || K.max_bounces <= 0) return false;
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    const bool hit_lds = (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
+    rt_kparams L = K;
+    L.rec = nullptr;
+    const size_t lds = rt_render_lds_bytes(L, 256, hit_lds, true);
+    const long groups = (long)(160 * 1024) / (long)(lds ? lds : 1);  // 256-lane groups per CU: 1 wave per SIMD each
+    return groups < RT_WAVES_PER_EU;
+}
+
+// Floats of a global-memory record stack for one launch: 3 * max_bounces
+// planes over the grid's lanes (the grid covers every work item, rounded up
+// to the largest workgroup).
+size_t rt_render_rec_floats(const rt_kparams& K) {
+    long nitems = (long)K.rows * K.width;
+    if (K.tile_w > 0) {
+        const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
+        nitems = tiles_x * tiles_y * 64;
+    }
+    return (size_t)3 * K.max_bounces * (size_t)((nitems + 255) / 256 * 256);
+}
 
 // LDS bytes of one workgroup: hit table (if staged) + 3 record dwords per
 // level per lane (+ 13 task-slot dwords per lane and 4 counters, sorted).
@@ -1556,7 +1598,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
-    size_t b = hit + (size_t)3 * (K.max_bounces + (sorted ? 0 : 1)) * block * sizeof(float);
+    size_t b = hit + (sorted && K.rec ? 0 : (size_t)3 * (K.max_bounces + (sorted ? 0 : 1)) * block * sizeof(float));
 #ifdef RT_MAILBOX
     if (sorted) b += (size_t)23 * block * sizeof(float) + 4 * sizeof(int);
 #else

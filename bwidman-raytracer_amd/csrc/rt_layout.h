@@ -80,6 +80,11 @@ struct rt_kparams {
     // conservative polygon culling (see polygon_test): only rays whose origin
     // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
     float cull_omax;
+    // recursion record stack in global memory (sorted kernel, deep paths):
+    // 3 * max_bounces planes of rec_stride floats ([field][level][lane]);
+    // null = records in LDS
+    float* rec;
+    int rec_stride;             // lanes in the grid (set by the launcher)
 };
 
 // Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,
