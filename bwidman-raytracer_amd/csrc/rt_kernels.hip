@@ -1634,6 +1634,11 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
             return launch_block<256, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
         }
     }
+    // BVH traversal: node-loop lengths differ widely between waves and a
+    // group waits for its slowest wave at every round's barriers, so the BVH
+    // kernels run single-wave groups (config 5: 246 -> 215 ms; 128 lanes: 226)
+    if (K.bvh_nodes) return launch_block<64, true>(K, hit_lds, rt_render_lds_bytes(K, 64, hit_lds, true), grid_mult,
+                                                   num_cus, stream);
     const size_t lds_s = rt_render_lds_bytes(K, RT_SORTED_BLOCK, hit_lds, true);
     // deep paths (large max_bounces) make the LDS record stack big: take
     // 128-lane groups when they keep more waves resident per CU (LDS 160 KB,
