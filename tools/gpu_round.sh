@@ -7,7 +7,7 @@ set -o pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 600 python -m pytest tests -q -m gpu > $OUT/pytest_gpu.log 2>&1; echo "pytest_gpu rc=$?"; tail -2 $OUT/pytest_gpu.log
+timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; echo "pytest_gpu rc=$rc"; tail -2 $OUT/pytest_gpu.log; [ $rc = 0 ] || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; cat $OUT/smoke.log; exit 1; }
 cat $OUT/smoke.log
 timeout -k 10 300 python bench.py > $OUT/bench.log 2>&1 || { echo bench failed; tail -5 $OUT/bench.log; exit 1; }
