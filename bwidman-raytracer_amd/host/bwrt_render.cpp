@@ -34,6 +34,13 @@ static int die(rt_context* ctx, int rc, const char* what) {
     return 1;
 }
 
+static const char* kUsage =
+    "usage: bwrt_render [--scene 07|01|04|04_box | --scene-file FILE] [--save-scene FILE]\n"
+    "                   [--width 1920] [--height 1080] [--frames 8] [--frames-per-call 1]\n"
+    "                   [--max-bounces 5] [--background r,g,b] [--device 0] [--gpus 1]\n"
+    "                   [--keys \"W*10,W+LEFT*5,*3\"] [--dt SECONDS]\n"
+    "                   [--out image.png|image.ppm] [--dump-scene file.bin]\n";
+
 struct KeyStep {
     unsigned keys;
     int frames;
@@ -92,7 +99,10 @@ int main(int argc, char** argv) {
     double fixed_dt = -1.0;
     for (int i = 1; i < argc; i++) {
         auto next = [&](void) -> const char* { return i + 1 < argc ? argv[++i] : ""; };
-        if (!std::strcmp(argv[i], "--scene")) scene_name = next();
+        if (!std::strcmp(argv[i], "--help") || !std::strcmp(argv[i], "-h")) {
+            std::fputs(kUsage, stdout);
+            return 0;
+        } else if (!std::strcmp(argv[i], "--scene")) scene_name = next();
         else if (!std::strcmp(argv[i], "--scene-file")) scene_file = next();
         else if (!std::strcmp(argv[i], "--save-scene")) save = next();
         else if (!std::strcmp(argv[i], "--width")) width = std::atoi(next());
@@ -112,7 +122,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--out")) out = next();
         else if (!std::strcmp(argv[i], "--dump-scene")) dump = next();
         else {
-            std::fprintf(stderr, "unknown option %s\n", argv[i]);
+            std::fprintf(stderr, "unknown option %s\n%s", argv[i], kUsage);
             return 2;
         }
     }

@@ -107,3 +107,11 @@ def test_cpp_png_and_ppm_writers(tmp_path):
     a = np.frombuffer(raw.read_bytes(), np.uint8).reshape(257, 300, 4)
     assert np.array_equal(np.asarray(Image.open(png).convert("RGBA")), a[::-1])
     assert np.array_equal(np.asarray(Image.open(ppm).convert("RGB")), a[::-1, :, :3])
+
+
+def test_cli_usage():
+    """--help prints the usage and exits 0; an unknown option exits 2 with it."""
+    ok = subprocess.run([CLI, "--help"], capture_output=True, text=True, timeout=30)
+    assert ok.returncode == 0 and ok.stdout.startswith("usage: bwrt_render")
+    bad = subprocess.run([CLI, "--no-such-option"], capture_output=True, text=True, timeout=30)
+    assert bad.returncode == 2 and "unknown option --no-such-option" in bad.stderr and "usage:" in bad.stderr
