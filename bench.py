@@ -35,6 +35,15 @@ from bwrt import Renderer, abi, scenes  # noqa: E402
 from bwrt.dist import ShardPlan, gather_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# closest-hit queries (traced ray segments) per full frame, SURVEY.md §8(d)'s
+# "actual segments".  The paths are a deterministic function of the scene and
+# the RNG streams (bit-exact with the oracle): c2 / c3 are the oracle's count
+# for the first frame from the y*W+x seeds (tests/test_oracle.py checks
+# them), c4 / c5 the diagnostic build's count (-DRT_STAMPS,
+# tools/stamps_run.py, stamps[16]) for the stream's second frame.  Each bench
+# step continues the streams, so a step's count differs by < 0.1 % (c3:
+# 32,340,255 first frame, 32,347,861 second).
+QUERIES_PER_FRAME = {"c2": 6619930, "c3": 32340255, "c4": 261860320, "c5": 346188412}
 BYTES_PER_PIXEL_PASS = 76  # rng 24+24, frameSum 12+12, RGBA8 4
 
 
@@ -219,6 +228,9 @@ def main():
                        + (" (frames pipelined: gather of frame k overlaps render of k+1)" if overlap else "")},
             "ms_per_frame": round(ms_step, 4),
             "kernel_ms_avg": round(kern_avg_ms, 4),
+            "queries_per_frame": QUERIES_PER_FRAME.get(args.config),
+            "actual_Msegments_per_s": (round(QUERIES_PER_FRAME[args.config] * args.steps / elapsed / 1e6, 1)
+                                       if args.config in QUERIES_PER_FRAME else None),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (round(traffic["hbm_bytes_per_launch"]) if traffic else None),

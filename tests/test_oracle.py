@@ -136,3 +136,16 @@ def test_work_profile_counters(oracle):
     q, p = oracle.last_counters()
     assert p == 480 * 270 * 2
     assert 1.8 < q / p < 2.1
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_bench_query_counts(oracle, cfg):
+    """bench.py's actual-segment counts (closest-hit queries per full frame,
+    counted on the GPU by the diagnostic build) equal the oracle's own count
+    of the same frame: the paths are deterministic and bit-exact."""
+    import bench
+    key, W, H, SPP, MB, _ = scenes.CONFIGS[cfg]
+    oracle.render_image(scenes.SCENES[key](), W, H, SPP, MB)
+    q, p = oracle.last_counters()
+    assert p == W * H * SPP
+    assert q == bench.QUERIES_PER_FRAME[cfg]
