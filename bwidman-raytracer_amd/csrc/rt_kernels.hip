@@ -213,20 +213,13 @@ __device__ __forceinline__ float specular_weight(f3 i, f3 o, f3 n, f3 m, float r
 // scaling of a float, no under/overflow), so fma(float(u), 2^-31, -1) =
 // RN(RN(float(u) * 2^-31) - 1), bit-identical to the two-step reference.
 __device__ __forceinline__ float rand_pm1(Xorwow& s) {
-#ifdef RT_REJ_NOFMA
-    return rand_range(s, 2.0f) - 1.0f;
-#else
     return __builtin_fmaf((float)next_u32(s), 4.656612873077393e-10f, -1.0f);
-#endif
 }
 
 __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters = nullptr) {
     f3 r;
     // 5 trips = 15 XORWOW steps bring the 5-word state back to its registers:
     // unrolling by 5 removes the per-trip register rotation
-#ifdef RT_REJ_UNROLL
-#pragma unroll RT_REJ_UNROLL
-#endif
     do {
         if (iters) ++*iters;
         float x = rand_pm1(s);
@@ -241,30 +234,6 @@ __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters 
     if (dot(normal, r) < 0.0f) r = sub(r, scale(2.0f * dot(r, normal), normal));
     return r;
 }
-
-#ifdef RT_REJ_CAP
-// At most RT_REJ_CAP rejection trips per round: a task still rejecting is
-// handed back with its advanced RNG state and re-posted next round (the
-// candidate stream is memoryless in the state, so the accepted point is the
-// same one).  Returns false when not yet accepted.
-__device__ __forceinline__ bool random_direction_capped(Xorwow& s, f3 normal, f3& out) {
-    f3 r;
-    int trips = 0;
-    bool ok;
-    do {
-        float x = rand_pm1(s);
-        float y = rand_pm1(s);
-        float z = rand_pm1(s);
-        r = mk(x, y, z);
-        ok = !(r.x * r.x + r.y * r.y + r.z * r.z > 1.00000012f);
-    } while (!ok && ++trips < RT_REJ_CAP);
-    if (!ok) return false;
-    r = normalize3(r);
-    if (dot(normal, r) < 0.0f) r = sub(r, scale(2.0f * dot(r, normal), normal));
-    out = r;
-    return true;
-}
-#endif
 
 // ---- closest hit over the whole scene (Main.cu:217-234 + Intersection.cuh)
 // The loop index is wave-uniform: primitive fields are scalar loads.  Only
@@ -332,34 +301,6 @@ __device__ __forceinline__ bool culled(const __attribute__((address_space(4))) f
     return cr.ok && lhs > cs[3] * cr.a;
 }
 
-__device__ __forceinline__ bool culled4(float4 cs, const CullRay& cr, f3 o, f3 d) {
-    const float wx = cs.x - o.x, wy = cs.y - o.y, wz = cs.z - o.z;
-    const float ww = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
-    const float pj = __builtin_fmaf(wx, d.x, __builtin_fmaf(wy, d.y, wz * d.z));
-    const float lhs = __builtin_fmaf(-pj, pj, ww * cr.a_k);
-    return cr.ok && lhs > cs.w * cr.a;
-}
-
-// exact polygon test after the cull (Intersection.cuh:108-173)
-__device__ __forceinline__ void polygon_exact(const rt_kparams& K, const __attribute__((address_space(4))) float* q, int nv,
-                                              f3 o, f3 d, int id, float& best_t, int& best_id) {
-    RT_BRANCH_COUNT(K, 2);
-    float nx = q[0], ny = q[1], nz = q[2], dd = q[3];
-    float nd = nx * d.x + ny * d.y + nz * d.z;
-    if (!(fabsf(nd) < RT_NEAR_ZERO)) {
-        float t = -((nx * o.x + ny * o.y + nz * o.z) + dd) / nd;
-        bool plane_hit = !(t <= RT_NEAR_ZERO || t > INFINITY);
-        if (plane_hit && !(t <= RT_NEAR_ZERO || t > best_t)) {
-            RT_BRANCH_COUNT(K, 3);
-            f3 P = add(o, scale(t, d));
-            if (polygon_edges(q + 4, nv, P)) {
-                best_t = t;
-                best_id = id;
-            }
-        }
-    }
-}
-
 __device__ __forceinline__ void polygon_test(const rt_kparams& K, const __attribute__((address_space(4))) float* q, int nv,
                                              f3 o, f3 d, int id, const CullRay& cr, float& best_t, int& best_id) {
     if (culled(q + (nv == 3 ? RT_TRI_CULL : RT_QUAD_CULL), cr, o, d)) return;
@@ -401,61 +342,7 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
     const int quad_base = tri_base + K.n_tri;
     const CullRay cr = cull_ray(K, o, a);
     RT_BRANCH_COUNT(K, 4);
-#ifdef RT_PREFETCH
-    // software-pipelined scalar loads: the sphere, plane and triangle-cull
-    // records of iteration i+1 are requested while iteration i is tested
-    // (indices clamped: the last iteration re-reads its own record).
-    // Measured slower (0.996 vs 0.908 ms): the extra SGPRs spill (36 -> 55
-    // SGPRs spilled to VGPR lanes).
-    auto ld4 = [](cfloat_ptr p) { return make_float4(p[0], p[1], p[2], p[3]); };
-    const int ls = K.n_sph > 0 ? K.n_sph - 1 : 0, lp = K.n_pln > 0 ? K.n_pln - 1 : 0,
-              lt = K.n_tri > 0 ? K.n_tri - 1 : 0;
-    float4 sN = ld4(as_const(K.sph));
-    float4 pN = ld4(as_const(K.pln));
-    float4 cN = ld4(as_const(K.tri) + RT_TRI_CULL);
     for (int i = 0; i < K.n_max; i++) {
-        const float4 sC = sN, pC = pN, cC = cN;
-        sN = ld4(as_const(K.sph) + RT_SPH_FLOATS * min(i + 1, ls));
-        pN = ld4(as_const(K.pln) + RT_PLN_FLOATS * min(i + 1, lp));
-        cN = ld4(as_const(K.tri) + RT_TRI_FLOATS * min(i + 1, lt) + RT_TRI_CULL);
-        if (i < K.n_sph) {  // Intersection.cuh:15-62
-            f3 xp = mk(o.x - sC.x, o.y - sC.y, o.z - sC.z);
-            float b = 2.0f * dot(xp, d);
-            float c = dot(xp, xp) - sC.w;
-            float disc = b * b - a4 * c;
-            if (!(disc < 0.0f) && !(b >= 0.0f && disc == disc && a2 > 0.0f)) {
-                RT_BRANCH_COUNT(K, 0);
-                float t = (-b - sqrtf(disc)) / a2;
-                if (!(t <= RT_NEAR_ZERO || t > best_t)) {
-                    best_t = t;
-                    best_id = i;
-                }
-            }
-        }
-        if (i < K.n_pln) {  // Intersection.cuh:64-106
-            float nd = pC.x * d.x + pC.y * d.y + pC.z * d.z;
-            if (!(fabsf(nd) < RT_NEAR_ZERO)) {
-                float t = -((pC.x * o.x + pC.y * o.y + pC.z * o.z) + pC.w) / nd;
-                if (!(t <= RT_NEAR_ZERO || t > best_t)) {
-                    best_t = t;
-                    best_id = pln_base + i;
-                }
-            }
-        }
-        if (i < K.n_tri && !culled4(cC, cr, o, d))
-            polygon_exact(K, as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, best_t, best_id);
-        if (i < K.n_quad)
-            polygon_test(K, as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, cr, best_t, best_id);
-    }
-    return;
-#endif
-#ifdef RT_UNROLL_MAXN
-#pragma unroll
-    for (int i = 0; i < RT_UNROLL_MAXN; i++) {
-        if (i >= K.n_max) break;
-#else
-    for (int i = 0; i < K.n_max; i++) {
-#endif
         if (i < K.n_sph) {  // Intersection.cuh:15-62
             const cfloat_ptr s = as_const(K.sph) + RT_SPH_FLOATS * i;
             f3 xp = mk(o.x - s[0], o.y - s[1], o.z - s[2]);
@@ -740,9 +627,6 @@ struct PixelState {
 };
 
 __device__ __forceinline__ void load_pixel(const rt_kparams& K, long npix, long p, PixelState& s) {
-#ifdef RT_SCRAMBLE
-    if (p < npix) p = (p * 7919) % npix;  // coherence experiment only
-#endif
     s.p = p;
     s.valid = p < npix;
     s.passes_left = 0;
@@ -954,11 +838,7 @@ rt_render_kernel(rt_kparams K) {
         STAMP(4);
         // (1) regenerate: jittered camera ray (Main.cu:290-292)
         if (depth < 0 && px.passes_left > 0) {
-#ifdef RT_ABL_NOJITTER
-            f3 jit = px.d0;
-#else
             f3 jit = random_direction(px.rs, px.d0);
-#endif
             d = normalize3(add(px.d0, scale(K.jitter, jit)));
             o = cam;
             depth = 0;
@@ -990,15 +870,7 @@ rt_render_kernel(rt_kparams K) {
                 int code = id;
                 float kspec = 0.0f;
                 const float choice = rand_range(px.rs, 1.0f);
-#if defined(RT_ABL_NOSHADE)
-                if (false) {
-#elif defined(RT_ABL_ALLSPEC)
-                if (true) {
-#elif defined(RT_ABL_ALLDIFF)
-                if (false) {
-#else
                 if (choice < RT_SPECULAR_CHANCE) {
-#endif
                     // genMicrofacetNormal (Main.cu:170-185)
                     const float e1 = rand_range(px.rs, 1.0f);
                     const float e2 = rand_range(px.rs, 1.0f);
@@ -1022,11 +894,7 @@ rt_render_kernel(rt_kparams K) {
                     kspec = sw * fr / RT_SPECULAR_CHANCE;  // brdf = (s*F/0.5) * {1,1,1}
                     code = ~id;
                 } else {
-#if defined(RT_ABL_NOSHADE)
-                    scatter = sub(d, scale(2.0f * dot(d, n), n));
-#else
                     scatter = random_direction(px.rs, n);  // brdf = 4 * albedo
-#endif
                 }
                 (void)albedo;
                 rec_code[depth * BLOCK] = code;
@@ -1161,13 +1029,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     float* rec_k = rec_mem + levels * RS + tid;
     float* rec_c = rec_mem + 2 * levels * RS + tid;
     float* slots = GREC ? rec_base : rec_base + 3 * levels * BLOCK;
-#ifdef RT_MAILBOX
-    float* mbox = slots + 13 * BLOCK;  // task results: r.xyz, kspec, rng[6]
-    int* counters = reinterpret_cast<int*>(mbox + 10 * BLOCK);
-#define MBOX(f, i) mbox[(f) * BLOCK + (i)]
-#else
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
-#endif
     // counters[0..3]: queue fronts/backs (2 parities)
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
@@ -1178,13 +1040,9 @@ rt_render_sorted_kernel(rt_kparams K) {
 #endif
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
-// task results {r.xyz, kspec, rng[6]}: a separate mailbox (RT_MAILBOX), or
-// written back over the slot's own fields {0..3, 7..12}
-#ifdef RT_MAILBOX
-#define RES(f, i) MBOX(f, i)
-#else
+// task results {r.xyz, kspec, rng[6]}, written back over the slot's own
+// fields {0..3, 7..12}
 #define RES(f, i) slots[((f) < 4 ? (f) : (f) + 3) * BLOCK + (i)]
-#endif
 
     PixelState px;
     load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
@@ -1250,11 +1108,9 @@ rt_render_sorted_kernel(rt_kparams K) {
     while (true) {
         const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
         STAMP(7);
-#ifndef RT_MAILBOX
         // every owner has read its previous task result out of the slots
         // before any wave overwrites them with this round's tasks
         __syncthreads();
-#endif
         STAMP(0);
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
@@ -1295,15 +1151,6 @@ rt_render_sorted_kernel(rt_kparams K) {
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
         if (nf + nb == 0) break;
-#ifdef RT_MAILBOX
-        // next round's counters were last read before the previous round's
-        // second barrier; the barrier after the execute step orders this
-        // reset before any wave posts next round's tasks
-        if (tid == 0) {
-            counters[2 * (parity ^ 1)] = 0;
-            counters[2 * (parity ^ 1) + 1] = 0;
-        }
-#endif
 
         // ---- T-phase: execute slot `tid`
         {
@@ -1335,15 +1182,8 @@ rt_render_sorted_kernel(rt_kparams K) {
                 int* rej_ptr = nullptr;
 #endif
                 if (do_front) {
-#ifdef RT_REJ_CAP
-                    (void)rej_ptr;
-                    const bool done = random_direction_capped(rs, nrm, r);
-                    if (done && code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // Main.cu:291-292
-                    RES(3, tid) = done ? 0.0f : 1.0f;  // 1: still rejecting, re-post
-#else
                     r = random_direction(rs, nrm, rej_ptr);
                     if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
-#endif
                 } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
@@ -1384,12 +1224,10 @@ rt_render_sorted_kernel(rt_kparams K) {
 #endif
         __syncthreads();
         STAMP(4);
-#ifndef RT_MAILBOX
         if (tid == 0) {
             counters[2 * (parity ^ 1)] = 0;
             counters[2 * (parity ^ 1) + 1] = 0;
         }
-#endif
         parity ^= 1;
 
         // ---- owner: take the task result back
@@ -1401,11 +1239,6 @@ rt_render_sorted_kernel(rt_kparams K) {
             px.rs.v2 = __float_as_uint(RES(7, slot));
             px.rs.v3 = __float_as_uint(RES(8, slot));
             px.rs.v4 = __float_as_uint(RES(9, slot));
-#ifdef RT_REJ_CAP
-            if (task != T_SPEC && RES(3, slot) != 0.0f) {
-                // rejection sampling not finished: same task again next round
-            } else
-#endif
             {
             mode = M_IDLE;
             if (task == T_REGEN) {
@@ -1483,9 +1316,6 @@ rt_render_sorted_kernel(rt_kparams K) {
 #undef STAMP
 #undef SLOT
 #undef RES
-#ifdef RT_MAILBOX
-#undef MBOX
-#endif
 }
 
 // ---- launchers (host side) ------------------------------------------------
@@ -1599,11 +1429,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
     size_t b = hit + (sorted && K.rec ? 0 : (size_t)3 * (K.max_bounces + (sorted ? 0 : 1)) * block * sizeof(float));
-#ifdef RT_MAILBOX
-    if (sorted) b += (size_t)23 * block * sizeof(float) + 4 * sizeof(int);
-#else
     if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
-#endif
     return b;
 }
 
