@@ -487,3 +487,44 @@ def test_random_scenes(gpu, oracle, monkeypatch, seed):
     gpu.set_scene(scenes.scene_07())
     assert np.array_equal(img, st.rgba)
     same_state(gpu, st)
+
+
+def _fresh_renderer(bwrt_lib, monkeypatch, **env):
+    """A renderer created under BWRT_* launch knobs (read at rt_create)."""
+    from bwrt import Renderer
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    try:
+        return Renderer(0, lib=bwrt_lib)
+    finally:
+        for k in env:
+            monkeypatch.delenv(k)
+
+
+@pytest.mark.parametrize("block", [64, 128, 256])
+@pytest.mark.parametrize("w,h,mb", [(160, 90, 4), (100, 37, 6)])
+def test_global_records_forced(bwrt_lib, oracle, monkeypatch, block, w, h, mb):
+    """The sorted kernel with its recursion records in global memory
+    (BWRT_GREC=1; the launch policy picks it for deep paths such as config 4)
+    at every workgroup size, including ragged sizes and a row shard."""
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_GREC=1, BWRT_BLOCK=block)
+    try:
+        for off, stride in ((0, 1), (1, 3)):
+            img, st = run_pair(r, oracle, scenes.scene_07(), w, h, 3, mb, row_offset=off, row_stride=stride)
+            assert np.array_equal(img, st.rgba)
+            same_state(r, st)
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("name", ["07", "04_box"])
+def test_simple_kernel_ab_reference(bwrt_lib, oracle, monkeypatch, name):
+    """The one-path-per-lane kernel kept as the A/B reference (BWRT_KERNEL=simple)."""
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_KERNEL="simple")
+    scene = {"07": scenes.scene_07, "04_box": scenes.scene_04_box}[name]()
+    try:
+        img, st = run_pair(r, oracle, scene, 200, 113, 3, 5)
+        assert np.array_equal(img, st.rgba)
+        same_state(r, st)
+    finally:
+        r.close()
