@@ -775,6 +775,12 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 #endif
 // s_setprio of the wave that runs SPEC tasks during the execute step (the
 // longest wave there; measured 0.882 -> 0.876 ms); 0 disables
+// occupancy target of the sorted kernel with global-memory records (LDS no
+// longer bounds it): 7 waves/SIMD (config 4: 6.36 -> 6.08 ms vs the default
+// target; 8 spills and gains nothing)
+#ifndef RT_GREC_WAVES
+#define RT_GREC_WAVES 7
+#endif
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
 #endif
@@ -1002,7 +1008,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
 template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC && !BVH ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
     enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
     enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };
