@@ -876,6 +876,14 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
 }
 
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
+    K.tile_w = c->tile_w;
+    // deep paths: the sorted kernel's record stack in global memory (launch policy)
+    K.rec = nullptr;
+    if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {
+        const int rc = ensure_buf(c, c->rec, rt_render_rec_floats(K) * sizeof(float));
+        if (rc) return rc;
+        K.rec = (float*)c->rec.p;
+    }
     unsigned long long* stamps = nullptr;
     const int NST = 32;  // 8 per-phase wave-cycle sums + utilisation / branch counters
     if (std::getenv("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS)
@@ -889,12 +897,6 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         if (hipMalloc(&stamps, NGT * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemsetAsync(stamps, 0, NGT * sizeof(unsigned long long), s);
         K.stamps = stamps;
-    }
-    K.tile_w = c->tile_w;
-    K.rec = nullptr;
-    if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {
-        const size_t floats = rt_render_rec_floats(K);
-        if (ensure_buf(c, c->rec, floats * sizeof(float)) == RT_OK) K.rec = (float*)c->rec.p;
     }
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, s);
