@@ -1324,6 +1324,203 @@ rt_render_sorted_kernel(rt_kparams K) {
 #undef RES
 }
 
+#ifdef RT_TU_BVH
+// ---- BVH kernel with ray refill (large scenes) --------------------------------
+// One path per lane like rt_render_kernel, but the BVH walk is not a
+// wave-synchronous call: each lane keeps its walk state (node, parked leaf,
+// closest hit) across iterations, and once RT_REFILL lanes of a wave have
+// finished their walks, those lanes shade their hit and set up their next
+// ray while the others stay parked mid-walk (persistent traversal with ray
+// refill, Aila & Laine 2009), so the node loop runs on fuller waves instead
+// of waiting for each round's slowest ray.  A ray's tests and their
+// (t, RT_KEY) acceptance are exactly those of closest_hit_bvh (planes
+// first, then every primitive of every leaf whose inflated box the ray may
+// enter), so the result does not depend on when the lane walks.
+#ifndef RT_REFILL
+#define RT_REFILL 40
+#endif
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
+rt_render_bvh_refill_kernel(rt_kparams K) {
+    extern __shared__ float smem[];
+    const int tid = threadIdx.x;
+    const float* hit_tab = K.hit;
+    int* rec_code = reinterpret_cast<int*>(smem) + tid;
+    float* rec_k = smem + (K.max_bounces + 1) * BLOCK + tid;
+    float* rec_c = smem + 2 * (K.max_bounces + 1) * BLOCK + tid;
+    const long npix = (long)K.rows * K.width;
+    const long T = (long)gridDim.x * BLOCK;
+    const long nitems = items_of(K, npix);
+    PixelState px;
+    load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
+    const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
+    const float tiny = 1e-20f;
+
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+    int depth = -1;          // -1: the next ray is a camera ray
+    bool walking = false;    // a BVH walk is in flight
+    bool pending = false;    // a finished query waits to be shaded
+    bool idle = false;       // no pixel left
+    int node = -1, leaf = -1;
+    float best_t = INFINITY;
+    int best_id = -1, best_key = -1;
+    f3 inv = o, oinv = o;
+    float m = 0.0f, a2 = 0.0f, a4 = 0.0f;
+    const float* nodes = K.bvh_nodes;
+
+    while (true) {
+        // (A) lanes without a walk: shade the finished query, start the next ray
+        while (!walking && !idle) {
+            if (pending) {
+                pending = false;
+                bool finished = true;
+                if (best_id >= 0) {  // shade (Main.cu:237-264), as rt_render_kernel
+                    const float* h = hit_tab + RT_HIT_FLOATS * best_id;
+                    const float4 h0 = *reinterpret_cast<const float4*>(h);
+                    const float4 h2 = *reinterpret_cast<const float4*>(h + 8);
+                    const f3 P = add(o, scale(best_t, d));
+                    f3 n = mk(h0.x, h0.y, h0.z);
+                    if (h0.w != 0.0f) n = normalize3(sub(P, n));  // sphere: centre -> normal
+                    f3 scatter;
+                    int code = best_id;
+                    float kspec = 0.0f;
+                    const float choice = rand_range(px.rs, 1.0f);
+                    if (choice < RT_SPECULAR_CHANCE) {
+                        scatter = specular_scatter(px.rs, d, n, h2.x, h2.z, h2.y, kspec);
+                        code = ~best_id;
+                    } else {
+                        scatter = random_direction(px.rs, n);  // brdf = 4 * albedo
+                    }
+                    rec_code[depth * BLOCK] = code;
+                    rec_k[depth * BLOCK] = kspec;
+                    rec_c[depth * BLOCK] = dot(scatter, n);  // cosAngle, Main.cu:264
+                    depth++;
+                    o = P;
+                    d = scatter;
+                    finished = depth > K.max_bounces;  // Main.cu:210
+                }
+                if (finished) {  // fold (Main.cu:262-268), accumulate (Main.cu:299-304)
+                    float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];
+                    for (int l = depth - 1; l >= 0; --l)
+                        fold_level(rec_code[l * BLOCK], rec_k[l * BLOCK], rec_c[l * BLOCK], hit_tab, lx, ly, lz);
+                    if (px.frame == 1u) {
+                        px.ax = 0.0f;
+                        px.ay = 0.0f;
+                        px.az = 0.0f;
+                    }
+                    px.ax = px.ax + lx;
+                    px.ay = px.ay + ly;
+                    px.az = px.az + lz;
+                    px.frame++;
+                    px.passes_left--;
+                    depth = -1;
+                    if (px.passes_left == 0) {
+                        store_pixel(K, npix, px);
+                        load_item(K, npix, nitems, px.w + T, px);
+                    }
+                }
+            }
+            if (depth < 0) {
+                if (px.passes_left <= 0) {
+                    idle = true;
+                    break;
+                }
+                // jittered camera ray (Main.cu:290-292)
+                const f3 jit = random_direction(px.rs, px.d0);
+                d = normalize3(add(px.d0, scale(K.jitter, jit)));
+                o = cam;
+                depth = 0;
+            }
+            // set up the walk of (o, d): closest_hit_bvh's prologue
+            best_t = INFINITY;
+            best_id = -1;
+            best_key = -1;
+            const bool finite = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
+                                fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
+            if (!finite) {  // NaN/inf rays: the reference's interleaved loop
+                closest_hit_brute(K, o, d, best_t, best_id);
+                pending = true;
+                continue;
+            }
+            const float a = dot(d, d);
+            a4 = 4.0f * a;
+            a2 = 2.0f * a;
+            for (int i = 0; i < K.n_pln; i++) {  // planes are unbounded: always tested
+                const cfloat_ptr q = as_const(K.pln) + RT_PLN_FLOATS * i;
+                const float nd = q[0] * d.x + q[1] * d.y + q[2] * d.z;
+                if (!(fabsf(nd) < RT_NEAR_ZERO)) {
+                    const float t = -((q[0] * o.x + q[1] * o.y + q[2] * o.z) + q[3]) / nd;
+                    const int key = RT_KEY(1, i);
+                    if (key_accept(t, key, best_t, best_key)) {
+                        best_t = t;
+                        best_id = K.n_sph + i;
+                        best_key = key;
+                    }
+                }
+            }
+            const f3 dc = mk(fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x,
+                             fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y,
+                             fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z);
+            inv = mk(1.0f / dc.x, 1.0f / dc.y, 1.0f / dc.z);
+            oinv = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+            m = 1e-6f + 9.5367431640625e-07f * fmaxf(fmaxf(fabsf(oinv.x), fabsf(oinv.y)), fabsf(oinv.z));
+            const int order = ((d.x < 0.0f) | ((d.y < 0.0f) << 1) | ((d.z < 0.0f) << 2)) & K.bvh_order_mask;
+            nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
+            node = 0;
+            leaf = -1;
+            walking = true;
+        }
+        if (__ballot(walking) == 0ull) break;  // every lane idle
+
+        // (B) walk until RT_REFILL lanes are waiting for a new ray
+        while (true) {
+            while (true) {  // node steps; a lane parks the first leaf its ray enters
+                bool stalled = false;
+                if (walking && node >= 0) {
+                    RT_BRANCH_COUNT(K, 5);
+                    const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
+                    const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
+                    const float tx0 = __builtin_fmaf(lo.x, inv.x, -oinv.x), tx1 = __builtin_fmaf(hi.x, inv.x, -oinv.x);
+                    const float ty0 = __builtin_fmaf(lo.y, inv.y, -oinv.y), ty1 = __builtin_fmaf(hi.y, inv.y, -oinv.y);
+                    const float tz0 = __builtin_fmaf(lo.z, inv.z, -oinv.z), tz1 = __builtin_fmaf(hi.z, inv.z, -oinv.z);
+                    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+                    const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+                    const bool hit = tmin <= tmax * (1.0f + 1e-5f) + m && tmin <= best_t * (1.0f + 1e-5f) + (1e-5f + m);
+                    const int miss = __float_as_int(lo.w);
+                    const int lf = __float_as_int(hi.w);
+                    if (!hit) {
+                        node = miss;
+                    } else if (lf < 0) {
+                        node = node + 1;
+                    } else if (leaf < 0) {
+                        leaf = lf;
+                        node = miss;
+                    } else {
+                        stalled = true;
+                    }
+                }
+                if (__all(!walking || leaf >= 0 || node < 0 || stalled)) break;
+            }
+            if (leaf >= 0) {
+                const int first = leaf & 0xffffff, count = leaf >> 24;
+                for (int k = 0; k < count; k++) {
+                    RT_BRANCH_COUNT(K, 6);
+                    leaf_test(K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
+                              best_key);
+                }
+                leaf = -1;
+            }
+            if (walking && node < 0) {  // walk complete: the query result is best_t / best_id
+                walking = false;
+                pending = true;
+            }
+            const unsigned long long w = __ballot(walking);
+            if (w == 0ull || __popcll(__ballot(!walking && !idle)) >= RT_REFILL) break;
+        }
+    }
+}
+#endif  // RT_TU_BVH
+
 // ---- launchers (host side) ------------------------------------------------
 namespace {
 template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC>
@@ -1366,6 +1563,20 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
 // The BVH instantiations live in their own translation unit
 // (rt_kernels_bvh.hip), built at -O3: the traversal loops want the full
 // optimizer while the brute-force kernels are faster at -O1.
+// BVH scenes by default: the ray-refill kernel, 64-lane groups (no barriers)
+hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, hipStream_t s) {
+    constexpr int BLOCK = 64;
+    long nitems = (long)K.rows * K.width;
+    if (K.tile_w > 0) {
+        const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
+        nitems = tiles_x * tiles_y * 64;
+    }
+    const long grid = (nitems + BLOCK - 1) / BLOCK;
+    const size_t lds = (size_t)3 * (K.max_bounces + 1) * BLOCK * sizeof(float);
+    hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(BLOCK), lds, s, K);
+    return hipGetLastError();
+}
+
 hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
                                 hipStream_t s) {
     const bool grec = sorted && K.rec;
@@ -1384,6 +1595,7 @@ hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, siz
 #else
 hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
                                 hipStream_t s);
+hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, hipStream_t s);
 
 namespace {
 template <int BLOCK, bool SORTED>
@@ -1445,7 +1657,8 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 // always covers every item); for the simple kernel grid_mult > 0 caps the
 // grid at grid_mult x resident workgroups per CU (persistent lanes).
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
-                            hipStream_t stream) {
+                            bool bvh_refill, hipStream_t stream) {
+    if (K.bvh_nodes && bvh_refill && !simple && block_req == 0) return rt_launch_render_bvh_refill(K, stream);
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = !K.bvh_nodes && (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
     const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 49152;

@@ -528,3 +528,20 @@ def test_simple_kernel_ab_reference(bwrt_lib, oracle, monkeypatch, name):
         same_state(r, st)
     finally:
         r.close()
+
+
+@pytest.mark.parametrize("name", ["stress", "07"])
+def test_bvh_through_sorted_kernel(bwrt_lib, oracle, monkeypatch, name):
+    """BVH scenes through the sorted task-queue kernel (BWRT_BVH_REFILL=0)
+    instead of the default ray-refill kernel; the 07 scene with the BVH
+    forced (shared pyramid edges: exact ties)."""
+    monkeypatch.setenv("BWRT_BVH_MIN", "1")
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_BVH_REFILL=0)
+    scene, w, h, mb = ((scenes.stress_scene(), 96, 54, 8) if name == "stress" else (scenes.scene_07(), 200, 113, 5))
+    try:
+        img, st = run_pair(r, oracle, scene, w, h, 2, mb)
+        assert np.array_equal(img, st.rgba)
+        same_state(r, st)
+    finally:
+        monkeypatch.delenv("BWRT_BVH_MIN")
+        r.close()
