@@ -1488,16 +1488,13 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                     const bool hit = tmin <= tmax * (1.0f + 1e-5f) + m && tmin <= best_t * (1.0f + 1e-5f) + (1e-5f + m);
                     const int miss = __float_as_int(lo.w);
                     const int lf = __float_as_int(hi.w);
-                    if (!hit) {
-                        node = miss;
-                    } else if (lf < 0) {
-                        node = node + 1;
-                    } else if (leaf < 0) {
-                        leaf = lf;
-                        node = miss;
-                    } else {
-                        stalled = true;
-                    }
+                    // branch-free step: miss -> skip the subtree; internal -> first
+                    // child; leaf -> park it (or stall on a second one)
+                    const bool is_leaf = hit && lf >= 0;
+                    stalled = is_leaf && leaf >= 0;
+                    const bool park = is_leaf && leaf < 0;
+                    leaf = park ? lf : leaf;
+                    node = !hit || park ? miss : (is_leaf ? node : node + 1);
                 }
                 if (__all(!walking || leaf >= 0 || node < 0 || stalled)) break;
             }
