@@ -24,7 +24,7 @@
 
 size_t rt_render_rec_floats(const rt_kparams& K);
 bool rt_render_wants_global_records(const rt_kparams& K);
-hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req, bool bvh_refill, bool sm,
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req, bool bvh_refill,
                             hipStream_t stream);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
                                hipStream_t stream);
@@ -71,7 +71,6 @@ struct rt_context {
     int num_cus = 256;
     bool simple = false;  // BWRT_KERNEL=simple: one-path-per-lane kernel (A/B reference)
     bool bvh_refill = true;  // BWRT_BVH_REFILL=0: BVH scenes through the sorted kernel instead
-    bool sm = false;         // BWRT_SM=1: brute-force scenes through the state-machine kernel
     int grid_mult = 0;  // persistent grid = grid_mult x resident workgroups per CU x CUs
     hipStream_t stream = nullptr;
     hipStream_t last_stream = nullptr;
@@ -491,7 +490,6 @@ int rt_create(int device, rt_context** out) {
     }
     if (const char* g = std::getenv("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
     if (const char* g = std::getenv("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
-    if (const char* g = std::getenv("BWRT_SM")) c->sm = std::atoi(g) != 0;
     *out = c;
     return RT_OK;
 }
@@ -903,7 +901,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.stamps = stamps;
     }
     HIP_TRY(c, hipEventRecord(c->ev0, s));
-    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, c->sm, s);
+    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, s);
     if (gtimes && stamps) {
         std::vector<unsigned long long> h(NGT);
         (void)hipMemcpyAsync(h.data(), stamps, NGT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);

@@ -218,6 +218,8 @@ __device__ __forceinline__ float rand_pm1(Xorwow& s) {
 
 __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters = nullptr) {
     f3 r;
+    // 5 trips = 15 XORWOW steps bring the 5-word state back to its registers:
+    // unrolling by 5 removes the per-trip register rotation
     do {
         if (iters) ++*iters;
         float x = rand_pm1(s);
@@ -944,135 +946,6 @@ rt_render_kernel(rt_kparams K) {
 }
 
 #ifndef RT_TU_BVH  // defined once, in the main translation unit
-// ---- per-lane state machine kernel (brute-force scenes) ---------------------
-// One path per lane, no task queue and no barriers.  Each lane is in one of
-// three states — DIR (a genRandomDirection in progress: the camera jitter or
-// a diffuse bounce), HIT (a ray waiting for its closest hit), SPEC (a
-// specular sample waiting) — and every iteration the wave runs ONE phase for
-// the lanes in that state: one rejection trip for the DIR lanes (cheap, so
-// it runs whenever nothing else is ready), or the closest hit / the specular
-// sample once enough lanes wait for it (RT_SM_HIT / RT_SM_SPEC), so the
-// expensive phases run on fuller waves and the rejection loop no longer
-// waits for the slowest lane of a round.  Each lane's own sequence of
-// operations and RNG draws is exactly rt_render_kernel's.
-#ifndef RT_SM_HIT
-#define RT_SM_HIT 40
-#endif
-#ifndef RT_SM_SPEC
-#define RT_SM_SPEC 24
-#endif
-template <int BLOCK>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
-rt_render_sm_kernel(rt_kparams K) {
-    enum { S_IDLE = 0, S_DIR = 1, S_HIT = 2, S_SPEC = 3 };
-    extern __shared__ float smem[];
-    const int tid = threadIdx.x;
-    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
-    for (int i = tid; i < n_prim * RT_HIT_FLOATS; i += BLOCK) smem[i] = K.hit[i];
-    __syncthreads();
-    const float* hit_tab = smem;
-    float* rec_base = smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3);
-    int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
-    float* rec_k = rec_base + (K.max_bounces + 1) * BLOCK + tid;
-    float* rec_c = rec_base + 2 * (K.max_bounces + 1) * BLOCK + tid;
-    const long npix = (long)K.rows * K.width;
-    const long T = (long)gridDim.x * BLOCK;
-    const long nitems = items_of(K, npix);
-    PixelState px;
-    load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
-    const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
-
-    int st = px.passes_left > 0 ? S_DIR : S_IDLE;
-    bool dir_cam = true;      // DIR: camera jitter (else a diffuse bounce)
-    f3 o = cam, d = px.d0;    // ray (HIT), incoming direction (SPEC)
-    f3 hP = o, hn = px.d0;    // pending hit point / normal (DIR diffuse, SPEC); hn = d0 for the jitter
-    int hid = 0, depth = 0;
-
-    // path end: fold (Main.cu:262-268), accumulate (Main.cu:299-304), next frame
-    auto finish = [&]() {
-        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];
-        for (int l = depth - 1; l >= 0; --l)
-            fold_level(rec_code[l * BLOCK], rec_k[l * BLOCK], rec_c[l * BLOCK], hit_tab, lx, ly, lz);
-        if (px.frame == 1u) {
-            px.ax = 0.0f;
-            px.ay = 0.0f;
-            px.az = 0.0f;
-        }
-        px.ax = px.ax + lx;
-        px.ay = px.ay + ly;
-        px.az = px.az + lz;
-        px.frame++;
-        px.passes_left--;
-        if (px.passes_left == 0) {
-            store_pixel(K, npix, px);
-            load_item(K, npix, nitems, px.w + T, px);
-        }
-        st = px.passes_left > 0 ? S_DIR : S_IDLE;
-        dir_cam = true;
-        hn = px.d0;
-    };
-    // a bounce's scatter direction is known: record it, continue or end (Main.cu:210, 264)
-    auto bounce = [&](int code, float kspec, f3 scatter) {
-        rec_code[depth * BLOCK] = code;
-        rec_k[depth * BLOCK] = kspec;
-        rec_c[depth * BLOCK] = dot(scatter, hn);
-        depth++;
-        o = hP;
-        d = scatter;
-        st = S_HIT;
-        if (depth > K.max_bounces) finish();
-    };
-
-    while (true) {
-        const int nh = __popcll(__ballot(st == S_HIT));
-        const int ns = __popcll(__ballot(st == S_SPEC));
-        const int nd = __popcll(__ballot(st == S_DIR));
-        if (nh + ns + nd == 0) break;
-        if (nh >= RT_SM_HIT || (nd == 0 && ns < RT_SM_SPEC && nh > 0)) {
-            if (st == S_HIT) {  // closest hit + brdfChoice (Main.cu:214-245)
-                float t;
-                int id;
-                closest_hit_brute(K, o, d, t, id);
-                if (id >= 0) {
-                    const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
-                    hP = add(o, scale(t, d));
-                    hn = mk(h0.x, h0.y, h0.z);
-                    if (h0.w != 0.0f) hn = normalize3(sub(hP, hn));  // sphere: centre -> normal
-                    hid = id;
-                    const bool spec = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE;
-                    st = spec ? S_SPEC : S_DIR;
-                    dir_cam = false;
-                } else {
-                    finish();
-                }
-            }
-        } else if (ns >= RT_SM_SPEC || (nd == 0 && ns > 0)) {
-            if (st == S_SPEC) {  // Main.cu:245-255
-                const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * hid + 8);
-                float kspec;
-                const f3 scatter = specular_scatter(px.rs, d, hn, h2.x, h2.z, h2.y, kspec);
-                bounce(~hid, kspec, scatter);
-            }
-        } else if (st == S_DIR) {  // one rejection trip of genRandomDirection (Main.cu:193-206)
-            const float x = rand_pm1(px.rs);
-            const float y = rand_pm1(px.rs);
-            const float z = rand_pm1(px.rs);
-            if (!(x * x + y * y + z * z > 1.00000012f)) {
-                f3 r = normalize3(mk(x, y, z));
-                if (dot(hn, r) < 0.0f) r = sub(r, scale(2.0f * dot(r, hn), hn));
-                if (dir_cam) {  // jittered camera ray (Main.cu:290-292)
-                    o = cam;
-                    d = normalize3(add(px.d0, scale(K.jitter, r)));
-                    depth = 0;
-                    st = S_HIT;
-                } else {
-                    bounce(hid, 0.0f, r);  // brdf = 4 * albedo
-                }
-            }
-        }
-    }
-}
-
 // initializeRand (Main.cu:369-380): curand_init(y*W + x, 0, 0)
 __global__ void __launch_bounds__(256) rt_init_rand_kernel(unsigned* rng, int width, int rows,
                                                            int row_offset, int row_stride) {
@@ -1781,25 +1654,8 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 // always covers every item); for the simple kernel grid_mult > 0 caps the
 // grid at grid_mult x resident workgroups per CU (persistent lanes).
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
-                            bool bvh_refill, bool sm, hipStream_t stream) {
+                            bool bvh_refill, hipStream_t stream) {
     if (K.bvh_nodes && bvh_refill && !simple && block_req == 0) return rt_launch_render_bvh_refill(K, stream);
-    {
-        const int np = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
-        if (sm && !K.bvh_nodes && (size_t)np * RT_HIT_FLOATS * sizeof(float) <= 16384) {
-            constexpr int BLOCK = 256;
-            long nitems = (long)K.rows * K.width;
-            if (K.tile_w > 0) {
-                const long tx = (K.width + K.tile_w - 1) / K.tile_w, ty = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
-                nitems = tx * ty * 64;
-            }
-            const long grid = (nitems + BLOCK - 1) / BLOCK;
-            const size_t lds = ((size_t)((np * RT_HIT_FLOATS + 3) & ~3) + (size_t)3 * (K.max_bounces + 1) * BLOCK) *
-                               sizeof(float);
-            hipLaunchKernelGGL((rt_render_sm_kernel<BLOCK>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(BLOCK), lds,
-                               stream, K);
-            return hipGetLastError();
-        }
-    }
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = !K.bvh_nodes && (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
     const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 49152;
