@@ -218,8 +218,6 @@ __device__ __forceinline__ float rand_pm1(Xorwow& s) {
 
 __device__ __forceinline__ f3 random_direction(Xorwow& s, f3 normal, int* iters = nullptr) {
     f3 r;
-    // 5 trips = 15 XORWOW steps bring the 5-word state back to its registers:
-    // unrolling by 5 removes the per-trip register rotation
     do {
         if (iters) ++*iters;
         float x = rand_pm1(s);
