@@ -98,7 +98,7 @@ struct rt_context {
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
     size_t host_rgba_bytes = 0;
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
-    int tile_w = 16;             // BWRT_TILE: wave tile width (16 x 4 pixel waves; 0 = linear order)
+    int tile_w = -1;             // BWRT_TILE: wave tile width (0 = linear order; -1 = launch policy)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
 };
@@ -878,7 +878,10 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
 }
 
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
-    K.tile_w = c->tile_w;
+    // wave tiles: 16 x 4 pixels; on small shards (one rank of a multi-GPU
+    // frame, below 1024 pixels per CU) 32 x 2 (config 3 at 1/8: 0.249 ->
+    // 0.244 ms; full frames: 16 x 4 0.871 vs 32 x 2 0.877 ms)
+    K.tile_w = c->tile_w >= 0 ? c->tile_w : ((long)K.rows * K.width <= (long)c->num_cus * 1024 ? 32 : 16);
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
     if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {

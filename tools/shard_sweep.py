@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--strides", default="1,2,4,8")
     ap.add_argument("--blocks", default="0,64,128,256")
-    ap.add_argument("--tiles", default="16")
+    ap.add_argument("--tiles", default="-1", help="wave tile widths; -1 = the library's launch policy")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     key, W, H, SPP, MB, _ = scenes.CONFIGS[a.config]
@@ -30,7 +30,10 @@ def main():
     for tile in [int(t) for t in a.tiles.split(",")]:
         for blk in [int(b) for b in a.blocks.split(",")]:
             os.environ["BWRT_BLOCK"] = str(blk)
-            os.environ["BWRT_TILE"] = str(tile)
+            if tile >= 0:
+                os.environ["BWRT_TILE"] = str(tile)
+            else:
+                os.environ.pop("BWRT_TILE", None)
             r = Renderer(0, lib=lib)
             r.set_scene(scenes.SCENES[key]())
             for g in [int(s) for s in a.strides.split(",")]:
