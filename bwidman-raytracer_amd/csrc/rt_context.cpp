@@ -880,8 +880,11 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
     // wave tiles: 16 x 4 pixels; on small shards (one rank of a multi-GPU
     // frame, below 1024 pixels per CU) 32 x 2 (config 3 at 1/8: 0.249 ->
-    // 0.244 ms; full frames: 16 x 4 0.871 vs 32 x 2 0.877 ms)
-    K.tile_w = c->tile_w >= 0 ? c->tile_w : ((long)K.rows * K.width <= (long)c->num_cus * 1024 ? 32 : 16);
+    // 0.244 ms; full frames: 16 x 4 0.871 vs 32 x 2 0.877 ms); BVH scenes
+    // 8 x 8 (4 x 16 on small shards): squarer tiles keep a wave's rays closer
+    // together in the tree (config 5: 170.4 -> 167.7 ms; at 1/8 38.5 -> 35.2)
+    const bool small = (long)K.rows * K.width <= (long)c->num_cus * 1024;
+    K.tile_w = c->tile_w >= 0 ? c->tile_w : K.bvh_nodes ? (small ? 4 : 8) : (small ? 32 : 16);
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
     if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {
