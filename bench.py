@@ -143,8 +143,9 @@ def main():
     nbuf = 2 if overlap else 1
     local_imgs = [torch.zeros(rows_per * W, dtype=torch.int32, device=dev) for _ in range(nbuf)]
     full_img = torch.empty(H * W, dtype=torch.int32, device=dev) if rank == 0 else None
+    # the gather's landing buffers exist on the root only
     gathered = ([torch.empty((world, rows_per * W), dtype=torch.int32, device=dev) for _ in range(nbuf)]
-                if world > 1 else None)
+                if world > 1 and rank == 0 else [None] * nbuf)
     # a dedicated (non-null) stream: the kernel, its timing events and the
     # RCCL gather are all ordered on it (NULL would mean the context's own
     # stream in the C ABI)
@@ -224,7 +225,7 @@ def main():
             "config": {"workload": f"07_specular_BRDF {W}x{H} {SPP}spp {MB}-bounce (BASELINE configs[2])"
                        if args.config == "c3" else f"{args.config}: scene {scene_key} {W}x{H} {SPP}spp {MB}-bounce",
                        "scene": scene_key, "width": W, "height": H, "spp": SPP, "max_bounces": MB,
-                       "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} all_gather" if world > 1 else "")
+                       "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} gather" if world > 1 else "")
                        + (" (frames pipelined: gather of frame k overlaps render of k+1)" if overlap else "")},
             "ms_per_frame": round(ms_step, 4),
             "kernel_ms_avg": round(kern_avg_ms, 4),

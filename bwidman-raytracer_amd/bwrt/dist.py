@@ -5,9 +5,10 @@ independent (the RNG seed is the global pixel index, Main.cu:377), so a frame
 splits across G ranks by INTERLEAVED rows — rank r renders rows
 y = r, r+G, r+2G, ... — which balances cheap sky rows against expensive floor
 rows.  Frames (spp) are never split: a pixel's RNG stream is sequential across
-frames.  After the render the ranks exchange ONE message: an all_gather of
-equal-size RGBA8 row blocks (padded to ceil(H/G) rows) over RCCL/xGMI, and
-rank 0 de-interleaves the blocks into the image (a HIP kernel on the GPU path).
+frames.  After the render the ranks exchange ONE message: a gather of
+equal-size RGBA8 row blocks (padded to ceil(H/G) rows) to rank 0 over
+RCCL/xGMI, and rank 0 de-interleaves the blocks into the image (a HIP kernel
+on the GPU path).
 """
 from __future__ import annotations
 
@@ -54,22 +55,29 @@ def deinterleave_reference(gathered, plan: ShardPlan, width: int):
     return out
 
 
-def gather_rows(local_block, plan: ShardPlan, out=None, group=None):
-    """all_gather of every rank's padded row block (torch tensors, any
-    backend: RCCL on GPUs, gloo in the CPU tests) into `out`
-    ([world, *local_block.shape], allocated when None); returns `out`."""
+def gather_rows(local_block, plan: ShardPlan, out=None, group=None, dst: int = 0):
+    """Rooted gather of every rank's padded row block to rank `dst` (torch
+    tensors, any backend: RCCL on GPUs, gloo in the CPU tests) into `out`
+    ([world, *local_block.shape], allocated on `dst` when None).  Returns
+    `out` on `dst` and None elsewhere.
+
+    Only rank 0 needs the image, so this is a gather, not an all_gather: over
+    RCCL each peer's block reaches the root on its own xGMI link (grouped
+    send/recv), where a ring all_gather would move every block across all
+    G - 1 links and keep RCCL kernels busy on every rank while the next frame
+    renders."""
     import torch
     import torch.distributed as dist
-    if out is None:
+    root = dist.get_rank(group) == dst if group is not None else dist.get_rank() == dst
+    if root and out is None:
         out = torch.empty((plan.world,) + tuple(local_block.shape), dtype=local_block.dtype,
                           device=local_block.device)
-    if dist.get_backend(group) == "gloo":
-        if local_block.is_cuda:  # rehearsal of the GPU path over gloo: stage through the host
-            host = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_gather(list(host.unbind(0)), local_block.cpu(), group=group)
+    if dist.get_backend(group) == "gloo" and local_block.is_cuda:
+        # rehearsal of the GPU path over gloo: stage through the host
+        host = torch.empty((plan.world,) + tuple(local_block.shape), dtype=local_block.dtype) if root else None
+        dist.gather(local_block.cpu(), gather_list=list(host.unbind(0)) if root else None, dst=dst, group=group)
+        if root:
             out.copy_(host)
-        else:
-            dist.all_gather(list(out.unbind(0)), local_block, group=group)
     else:
-        dist.all_gather_into_tensor(out, local_block, group=group)
-    return out
+        dist.gather(local_block, gather_list=list(out.unbind(0)) if root else None, dst=dst, group=group)
+    return out if root else None

@@ -1,5 +1,5 @@
 """Multi-rank path on CPU (world_size 2, gloo): the interleaved-row shard
-plan, the padded all_gather of RGBA8 row blocks and the de-interleave that
+plan, the padded gather of RGBA8 row blocks to rank 0 and the de-interleave that
 bench.py runs over RCCL.  The per-rank renderer here is the oracle (a CPU
 stand-in for libbwrt on a GPU-less box); the GPU tests check that
 libbwrt's shards equal the full image row for row."""
@@ -36,6 +36,7 @@ def _worker(rank, world, port, w, h, spp, mb, q):
     block = np.zeros((plan.rows_per_shard, w), dtype=np.uint32)
     block[:plan.rows] = st.rgba.view(np.uint32).reshape(plan.rows, w)
     gathered = gather_rows(torch.from_numpy(block.view(np.int32)).reshape(-1), plan)
+    assert (gathered is None) == (rank != 0)
     if rank == 0:
         img = deinterleave_reference(gathered.numpy().view(np.uint32), plan, w)
         q.put(img.view(np.uint8).reshape(h, w, 4))
@@ -43,9 +44,9 @@ def _worker(rank, world, port, w, h, spp, mb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("h", [54, 55])
-def test_two_rank_gather_matches_single_render(oracle, h):
-    w, spp, mb, world = 96, 2, 4, 2
+@pytest.mark.parametrize("h,world", [(54, 2), (55, 2), (55, 3)])
+def test_multi_rank_gather_matches_single_render(oracle, h, world):
+    w, spp, mb = 96, 2, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
