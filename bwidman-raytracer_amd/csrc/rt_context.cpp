@@ -28,6 +28,7 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
                             hipStream_t stream);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
                                hipStream_t stream);
+extern thread_local long rt_order_groups_last;
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
                                   int shards, int rows_per_shard, hipStream_t stream);
 
@@ -94,6 +95,11 @@ struct rt_context {
     int width = 0, height = 0, row_offset = 0, row_stride = 1, rows = 0;
     DevBuf rng, accum, rgba;
     DevBuf rec;  // sorted kernel's record stack in global memory (deep paths)
+    // launch-order feedback (rt_layout.h): tile-group costs of the last
+    // launch and the order sorted from them, valid for a grid of order_n groups
+    DevBuf gcost, gorder;
+    long order_n = 0;
+    bool order_feedback = true;  // BWRT_ORDER=0: blockIdx order
     int grec = -1;  // BWRT_GREC: 1 / 0 force global / LDS records; -1 = launch policy
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
     size_t host_rgba_bytes = 0;
@@ -490,6 +496,7 @@ int rt_create(int device, rt_context** out) {
     }
     if (const char* g = std::getenv("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
     if (const char* g = std::getenv("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
+    if (const char* g = std::getenv("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
     *out = c;
     return RT_OK;
 }
@@ -504,6 +511,8 @@ void rt_destroy(rt_context* c) {
     free_buf(c->accum);
     free_buf(c->rgba);
     free_buf(c->rec);
+    free_buf(c->gcost);
+    free_buf(c->gorder);
     if (c->host_rgba) (void)hipHostFree(c->host_rgba);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -906,8 +915,24 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
             (void)hipMemsetAsync(stamps, 0, NGT * sizeof(unsigned long long), s);
         K.stamps = stamps;
     }
+    // launch-order feedback: room for a grid of 64-lane groups over the
+    // padded wave tiles (any block size needs fewer groups)
+    if (c->order_feedback && !c->simple) {
+        const size_t cap = ((size_t)K.width + 64) * ((size_t)K.rows + 64) / 64 + 1;
+        const void* before = c->gorder.p;
+        int rc = ensure_buf(c, c->gcost, cap * sizeof(unsigned));
+        if (!rc) rc = ensure_buf(c, c->gorder, cap * sizeof(int));
+        if (rc) return rc;
+        if (c->gorder.p != before) c->order_n = 0;  // fresh buffer: no order yet
+        K.group_cost = (unsigned*)c->gcost.p;
+        K.group_order = (int*)c->gorder.p;
+        K.order_n = c->order_n;
+        K.order_cap = (long)(c->gorder.bytes / sizeof(int));
+    }
+    rt_order_groups_last = 0;
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, s);
+    if (e == hipSuccess && rt_order_groups_last > 0) c->order_n = rt_order_groups_last;
     if (gtimes && stamps) {
         std::vector<unsigned long long> h(NGT);
         (void)hipMemcpyAsync(h.data(), stamps, NGT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);

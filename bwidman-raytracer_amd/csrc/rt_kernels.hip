@@ -945,6 +945,40 @@ rt_render_kernel(rt_kparams K) {
 
 #ifndef RT_TU_BVH  // defined once, in the main translation unit
 // initializeRand (Main.cu:369-380): curand_init(y*W + x, 0, 0)
+// Launch-order feedback: one workgroup turns the last launch's tile-group
+// durations into the next launch's order, most expensive first (longest
+// processing time first: the frame's last workgroups are then the cheap
+// ones, so the chip drains quickly).  Counting sort over 256 linear cost
+// buckets; the order within a bucket is whatever the LDS atomics give, which
+// is harmless: every pixel's result is independent of when its group runs.
+__global__ void __launch_bounds__(1024) rt_order_groups_kernel(const unsigned* __restrict__ cost,
+                                                               int* __restrict__ order, int n) {
+    __shared__ unsigned hist[256];
+    __shared__ unsigned cmax;
+    const int tid = threadIdx.x;
+    if (tid < 256) hist[tid] = 0;
+    if (tid == 0) cmax = 0;
+    __syncthreads();
+    unsigned m = 0;
+    for (int i = tid; i < n; i += 1024) m = max(m, cost[i]);
+    atomicMax(&cmax, m);
+    __syncthreads();
+    const unsigned long long span = (unsigned long long)cmax + 1;
+    auto bucket = [&](int i) { return 255 - (int)(((unsigned long long)cost[i] * 256) / span); };
+    for (int i = tid; i < n; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        unsigned run = 0;
+        for (int b = 0; b < 256; b++) {
+            const unsigned c = hist[b];
+            hist[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = i;
+}
+
 __global__ void __launch_bounds__(256) rt_init_rand_kernel(unsigned* rng, int width, int rows,
                                                            int row_offset, int row_stride) {
     const long npix = (long)rows * width;
@@ -1005,7 +1039,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 //
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
-template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC>
+template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC && !BVH ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
     enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
@@ -1048,8 +1082,15 @@ rt_render_sorted_kernel(rt_kparams K) {
 // fields {0..3, 7..12}
 #define RES(f, i) slots[((f) < 4 ? (f) : (f) + 3) * BLOCK + (i)]
 
+    // tile-group of this workgroup (launch-order feedback, rt_layout.h)
+    // (the start time is parked in group_cost[] itself: nothing stays live
+    // across the loop)
+    // ORDER: launch-order feedback instantiation (the pointers it needs after
+    // the loop cost SGPRs, so launches without feedback use the plain one)
+    const long group = ORDER && K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
+    if (ORDER && tid == 0) K.group_cost[group] = (unsigned)__builtin_amdgcn_s_memrealtime();
     PixelState px;
-    load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
+    load_item(K, npix, nitems, group * BLOCK + tid, px);
     int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -1307,6 +1348,18 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(6);
     }
     if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
+    // the loop exit is group-uniform (the round that posts no task), so one
+    // lane's clock after the loop closes the group's span
+    if (ORDER && tid == 0) {
+        // the pointers re-read from the kernel arguments (volatile), so they
+        // are not held in SGPRs across the loop
+        const volatile __attribute__((address_space(4))) rt_kparams* kp =
+            (const volatile __attribute__((address_space(4))) rt_kparams*)__builtin_amdgcn_kernarg_segment_ptr();
+        int* const ord = kp->group_order;
+        unsigned* const cost = kp->group_cost;
+        const long g = ord ? (long)__builtin_nontemporal_load(&ord[blockIdx.x]) : (long)blockIdx.x;
+        cost[g] = (unsigned)__builtin_amdgcn_s_memrealtime() - cost[g];
+    }
 #ifdef RT_GTIMES
     __syncthreads();
     if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1517,6 +1570,15 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
 #endif  // RT_TU_BVH
 
 // ---- launchers (host side) ------------------------------------------------
+#ifndef RT_ORDER_MIN_GEN
+#define RT_ORDER_MIN_GEN 1.5
+#endif
+// launch-order feedback: the grid of the last launch that sorted its
+// tile-group costs into group_order (0 = none; the context resets it before
+// each launch and keeps the value as the order's grid)
+extern thread_local long rt_order_groups_last;
+hipError_t rt_launch_order_groups(const unsigned* cost, int* order, long n, hipStream_t stream);
+
 namespace {
 template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC>
 void* kernel_ptr() {
@@ -1544,12 +1606,42 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     if (grid < 1) grid = 1;
     K.rec_stride = (int)(grid * BLOCK);
-    if (SORTED)
+    // launch-order feedback: only where the sorted grid covers every item
+    // once (group g <-> tile-group g) and the buffers hold the grid
+    // and only where the grid runs in more than RT_ORDER_MIN_GEN generations
+    // of resident groups: LPT order shortens the drain at the end of a
+    // multi-generation grid, while a grid that is resident all at once only
+    // gets its expensive groups packed onto the same CUs (c3 at 1/8: 0.264
+    // vs 0.243 ms with the order; 1/2: 0.493 vs 0.522)
+    bool feedback = SORTED && K.group_cost && K.group_order && grid <= K.order_cap;
+    if (feedback) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC>(), BLOCK,
+                                                         lds) != hipSuccess ||
+            per_cu <= 0)
+            per_cu = 1;
+        feedback = (double)grid > RT_ORDER_MIN_GEN * (double)per_cu * num_cus;
+    }
+    if (!feedback) {
+        K.group_cost = nullptr;
+        K.group_order = nullptr;
+    } else if (K.order_n != grid) {
+        K.group_order = nullptr;  // no order for this grid yet: blockIdx order
+    }
+    if (SORTED && feedback)
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, true>), dim3((unsigned)grid), dim3(BLOCK),
+                           lds, stream, K);
+    else if (SORTED)
         hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC>), dim3((unsigned)grid), dim3(BLOCK), lds,
                            stream, K);
     else
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && feedback) {
+        e = rt_launch_order_groups(K0.group_cost, K0.group_order, grid, stream);
+        if (e == hipSuccess) rt_order_groups_last = grid;
+    }
+    return e;
 }
 
 }  // namespace
@@ -1700,6 +1792,13 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
         return launch_block<128, true>(K, hit_lds, lds_128, grid_mult, num_cus, stream);
     }
     return launch_block<RT_SORTED_BLOCK, true>(K, hit_lds, lds_s, grid_mult, num_cus, stream);
+}
+
+thread_local long rt_order_groups_last = 0;
+
+hipError_t rt_launch_order_groups(const unsigned* cost, int* order, long n, hipStream_t stream) {
+    hipLaunchKernelGGL(rt_order_groups_kernel, dim3(1), dim3(1024), 0, stream, cost, order, (int)n);
+    return hipGetLastError();
 }
 
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,

@@ -85,6 +85,16 @@ struct rt_kparams {
     // null = records in LDS
     float* rec;
     int rec_stride;             // lanes in the grid (set by the launcher)
+    // launch-order feedback (sorted kernel): workgroup g renders tile-group
+    // group_order[g] (null = g itself; a permutation of the grid's groups,
+    // valid only when order_n equals this launch's grid) and writes that
+    // tile-group's duration to group_cost[]; the launcher then sorts the
+    // costs so the next launch starts the most expensive tile-groups first
+    // and the frame ends on cheap ones.  Null group_cost = feature off.
+    int* group_order;
+    unsigned* group_cost;
+    long order_n;               // grid the current group_order was built for (0 = none)
+    long order_cap;             // capacity of group_order / group_cost
 };
 
 // Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,

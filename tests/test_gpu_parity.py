@@ -545,3 +545,29 @@ def test_bvh_through_sorted_kernel(bwrt_lib, oracle, monkeypatch, name):
     finally:
         monkeypatch.delenv("BWRT_BVH_MIN")
         r.close()
+
+
+@pytest.mark.parametrize("scene_name,w,h,spp,mb", [("07", 1920, 1080, 2, 4), ("04", 1600, 1200, 2, 3)])
+def test_launch_order_feedback(bwrt_lib, oracle, monkeypatch, scene_name, w, h, spp, mb):
+    """Launch-order feedback (grids of several resident generations: each
+    launch records its tile-groups' durations and the next launch starts the
+    most expensive first): the first render runs in blockIdx order, the
+    following ones reordered — every one equals the oracle bit for bit, and
+    a progressive continuation under the new order does too."""
+    scene = scenes.SCENES[scene_name]()
+    st = oracle.OracleState(w, h)
+    oracle.render(scene, st, spp, mb, first_frame=1)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
+    try:
+        r.set_scene(scene)
+        for _ in range(3):
+            r.init_rand(w, h)
+            img = r.render(w, h, spp, mb, first_frame=1)
+            assert np.array_equal(img, st.rgba)
+            same_state(r, st)
+        oracle.render(scene, st, 1, mb)
+        img = r.render(w, h, 1, mb)
+        assert np.array_equal(img, st.rgba)
+        same_state(r, st)
+    finally:
+        r.close()
