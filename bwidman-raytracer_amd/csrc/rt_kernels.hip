@@ -948,35 +948,44 @@ rt_render_kernel(rt_kparams K) {
 // Launch-order feedback: one workgroup turns the last launch's tile-group
 // durations into the next launch's order, most expensive first (longest
 // processing time first: the frame's last workgroups are then the cheap
-// ones, so the chip drains quickly).  Counting sort over 256 linear cost
-// buckets; the order within a bucket is whatever the LDS atomics give, which
-// is harmless: every pixel's result is independent of when its group runs.
+// ones, so the chip drains quickly).  Counting sort over 512 logarithmic cost
+// buckets (exponent and top 4 mantissa bits of float(cost): 1/16-octave
+// steps, no max pass); the order within a bucket is whatever the LDS
+// atomics give, which is harmless: every pixel's result is independent of
+// when its group runs.
+__device__ __forceinline__ int order_bucket(unsigned cost) {
+    const int k = (int)(__float_as_uint((float)cost + 1.0f) >> 19) - (127 << 4);  // 0 .. 512
+    return 511 - min(k, 511);
+}
+
 __global__ void __launch_bounds__(1024) rt_order_groups_kernel(const unsigned* __restrict__ cost,
                                                                int* __restrict__ order, int n) {
-    __shared__ unsigned hist[256];
-    __shared__ unsigned cmax;
+    __shared__ unsigned hist[512];
+    __shared__ unsigned wsum[8];
     const int tid = threadIdx.x;
-    if (tid < 256) hist[tid] = 0;
-    if (tid == 0) cmax = 0;
+    if (tid < 512) hist[tid] = 0;
     __syncthreads();
-    unsigned m = 0;
-    for (int i = tid; i < n; i += 1024) m = max(m, cost[i]);
-    atomicMax(&cmax, m);
+    for (int i = tid; i < n; i += 1024) atomicAdd(&hist[order_bucket(cost[i])], 1u);
     __syncthreads();
-    const unsigned long long span = (unsigned long long)cmax + 1;
-    auto bucket = [&](int i) { return 255 - (int)(((unsigned long long)cost[i] * 256) / span); };
-    for (int i = tid; i < n; i += 1024) atomicAdd(&hist[bucket(i)], 1u);
-    __syncthreads();
-    if (tid == 0) {
-        unsigned run = 0;
-        for (int b = 0; b < 256; b++) {
-            const unsigned c = hist[b];
-            hist[b] = run;
-            run += c;
+    // exclusive scan of the 512 buckets: waves 0..7, one bucket per lane
+    unsigned v = 0, incl = 0;
+    if (tid < 512) {
+        v = hist[tid];
+        incl = v;
+        for (int m = 1; m < 64; m <<= 1) {
+            const unsigned u = __shfl_up(incl, m);
+            if ((tid & 63) >= m) incl += u;
         }
+        if ((tid & 63) == 63) wsum[tid >> 6] = incl;
     }
     __syncthreads();
-    for (int i = tid; i < n; i += 1024) order[atomicAdd(&hist[bucket(i)], 1u)] = i;
+    if (tid < 512) {
+        unsigned base = 0;
+        for (int w = 0; w < (tid >> 6); w++) base += wsum[w];
+        hist[tid] = base + incl - v;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) order[atomicAdd(&hist[order_bucket(cost[i])], 1u)] = i;
 }
 
 __global__ void __launch_bounds__(256) rt_init_rand_kernel(unsigned* rng, int width, int rows,
