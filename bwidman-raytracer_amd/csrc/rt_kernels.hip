@@ -779,6 +779,11 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 #ifndef RT_GREC_WAVES
 #define RT_GREC_WAVES 7
 #endif
+// global-record launches keep this many shallow record levels in LDS
+// (3 dwords per level per lane; 2 still fits 7 waves/SIMD of the sorted kernel)
+#ifndef RT_GREC_LDS_LEVELS
+#define RT_GREC_LDS_LEVELS 2
+#endif
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
 #endif
@@ -1068,14 +1073,20 @@ rt_render_sorted_kernel(rt_kparams K) {
     // the path in the round it is made, so it is folded straight from the
     // lane's own task slot (fields 4..6, free once the result is taken)
     const int levels = K.max_bounces;
-    // record stack: LDS [field][level][lane], or (GREC) the same layout in
-    // global memory over the grid's lanes, which leaves LDS to the task slots
+    // record stack: LDS [field][level][lane]; GREC: only the shallow levels
+    // 0 .. LL-1 in LDS, the deep ones (rarely reached) in global memory in
+    // the same layout over the grid's lanes (stride RS), so LDS leaves room
+    // for RT_GREC_WAVES waves and few records ever leave the CU
+    const int LL = GREC ? (levels < RT_GREC_LDS_LEVELS ? levels : RT_GREC_LDS_LEVELS) : levels;
     const int RS = GREC ? K.rec_stride : BLOCK;
-    float* rec_mem = GREC ? K.rec + (long)blockIdx.x * BLOCK : rec_base;
-    int* rec_code = reinterpret_cast<int*>(rec_mem) + tid;
-    float* rec_k = rec_mem + levels * RS + tid;
-    float* rec_c = rec_mem + 2 * levels * RS + tid;
-    float* slots = GREC ? rec_base : rec_base + 3 * levels * BLOCK;
+    int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
+    float* rec_k = rec_base + LL * BLOCK + tid;
+    float* rec_c = rec_base + 2 * LL * BLOCK + tid;
+    float* grec_mem = GREC ? K.rec + (long)blockIdx.x * BLOCK : rec_base;
+    int* grec_code = reinterpret_cast<int*>(grec_mem) + tid;
+    float* grec_k = grec_mem + levels * RS + tid;
+    float* grec_c = grec_mem + 2 * levels * RS + tid;
+    float* slots = rec_base + 3 * LL * BLOCK;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
     // counters[0..3]: queue fronts/backs (2 parities)
     const long npix = (long)K.rows * K.width;
@@ -1114,7 +1125,11 @@ rt_render_sorted_kernel(rt_kparams K) {
         float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
         if (depth > K.max_bounces)  // deepest level, parked in the slot
             fold_level(__float_as_int(SLOT(6, slot)), SLOT(4, slot), SLOT(5, slot), hit_tab, lx, ly, lz);
-        fold_records(rec_code, rec_k, rec_c, RS, depth > K.max_bounces ? K.max_bounces : depth, hit_tab, lx, ly, lz);
+        const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
+        if (GREC)
+            for (int l = nrec - 1; l >= LL; --l)
+                fold_level(grec_code[l * RS], grec_k[l * RS], grec_c[l * RS], hit_tab, lx, ly, lz);
+        fold_records(rec_code, rec_k, rec_c, BLOCK, nrec < LL ? nrec : LL, hit_tab, lx, ly, lz);
         if (px.frame == 1u) {
             px.ax = 0.0f;
             px.ay = 0.0f;
@@ -1305,9 +1320,15 @@ rt_render_sorted_kernel(rt_kparams K) {
                 const float kspec = task == T_SPEC ? RES(3, slot) : 0.0f;
                 const float cosang = dot(r, hn);  // cosAngle, Main.cu:264
                 if (depth < K.max_bounces) {
-                    rec_code[depth * RS] = code;
-                    rec_k[depth * RS] = kspec;
-                    rec_c[depth * RS] = cosang;
+                    if (!GREC || depth < LL) {
+                        rec_code[depth * BLOCK] = code;
+                        rec_k[depth * BLOCK] = kspec;
+                        rec_c[depth * BLOCK] = cosang;
+                    } else {
+                        grec_code[depth * RS] = code;
+                        grec_k[depth * RS] = kspec;
+                        grec_c[depth * RS] = cosang;
+                    }
                     o = hP;
                     d = r;
                     has_ray = true;
@@ -1742,7 +1763,9 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
-    size_t b = hit + (sorted && K.rec ? 0 : (size_t)3 * (K.max_bounces + (sorted ? 0 : 1)) * block * sizeof(float));
+    const int lds_levels = sorted && K.rec ? (K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS)
+                                           : K.max_bounces + (sorted ? 0 : 1);
+    size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * block * sizeof(float);
     if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
     return b;
 }
