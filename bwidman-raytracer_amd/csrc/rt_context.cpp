@@ -74,8 +74,12 @@ struct rt_context {
     bool bvh_refill = true;  // BWRT_BVH_REFILL=0: BVH scenes through the sorted kernel instead
     int grid_mult = 0;  // persistent grid = grid_mult x resident workgroups per CU x CUs
     hipStream_t stream = nullptr;
-    hipStream_t last_stream = nullptr;
+    hipStream_t last_stream = nullptr;  // stream of the last launch (a caller's, via rt_render_device)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // end of the last render launch on `render_stream`: a launch on another
+    // stream waits for it (the kernels read and write the same shard state)
+    hipEvent_t ev_render = nullptr;
+    hipStream_t render_stream = nullptr;
     bool timed = false;
     std::string err;
 
@@ -140,8 +144,25 @@ void free_buf(DevBuf& b) {
     b.bytes = 0;
 }
 
+// Host-side writes of context state (scene, RNG seeds, frameSum, checkpoint
+// restore) and buffer reallocation must not overlap a render still running
+// on a caller's stream (rt_render_device): wait for that stream first.
+// Work on c->stream is already ordered by the stream itself.
+int quiesce(rt_context* c) {
+    if (c->last_stream && c->last_stream != c->stream) {
+        HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+        c->last_stream = c->stream;
+    }
+    return RT_OK;
+}
+
 int ensure_buf(rt_context* c, DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return RT_OK;
+    if (b.p) {  // the old buffer may still be in use by queued work
+        int rc = quiesce(c);
+        if (rc) return rc;
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
     free_buf(b);
     if (bytes == 0) return RT_OK;
     HIP_TRY(c, hipMalloc(&b.p, bytes));
@@ -479,7 +500,8 @@ int rt_create(int device, rt_context** out) {
     rt_context* c = new rt_context();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_render, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return RT_ERR_HIP;
     }
@@ -516,6 +538,7 @@ void rt_destroy(rt_context* c) {
     if (c->host_rgba) (void)hipHostFree(c->host_rgba);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_render) (void)hipEventDestroy(c->ev_render);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -595,6 +618,9 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
         if (const char* e = std::getenv("BWRT_BVH_MIN")) bvh_min = std::atoi(e);
         const int nb = ns + nt + nq;
         if (nb > 0 && nb >= bvh_min) {
+            // leaf encoding: 24-bit index of a leaf's first primitive record
+            if (nb >= (1 << 24))
+                return fail(c, RT_ERR_UNSUPPORTED, "%d bounded primitives: the BVH holds at most 2^24 - 1", nb);
             BvhBuilder B;
             B.items.reserve(nb);
             for (int i = 0; i < ns; i++) {
@@ -618,7 +644,9 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             for (int i = 0; i < nt; i++) poly(ns + np + i, s->triangles[i].vertices, 3);
             for (int i = 0; i < nq; i++) poly(ns + np + nt + i, s->quads[i].vertices, 4);
             B.tree.reserve(2 * (size_t)nb);
-            if (const char* e = std::getenv("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 255);
+            // leaf = (count << 24) | first in an int: count <= 127 keeps the sign
+            // bit clear (a negative value means "internal node" to the kernels)
+            if (const char* e = std::getenv("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 127);
             if (const char* e = std::getenv("BWRT_BVH_CT")) B.trav_cost = (float)std::atof(e);
             if (const char* e = std::getenv("BWRT_BVH_ORDER_MASK")) B.order_mask = std::atoi(e) & 7;
             B.build(0, nb);
@@ -652,7 +680,8 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
         }
     }
     const size_t bytes = h.size() * sizeof(float);
-    int rc = ensure_buf(c, c->scene_buf, bytes);
+    int rc = quiesce(c);  // a render on a caller's stream may still read the scene
+    if (!rc) rc = ensure_buf(c, c->scene_buf, bytes);
     if (rc) return rc;
     HIP_TRY(c, hipMemcpyAsync(c->scene_buf.p, h.data(), bytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -797,7 +826,8 @@ int rt_init_rand(rt_context* c, int width, int height, int row_offset, int row_s
     HIP_TRY(c, hipSetDevice(c->device));
     const int rows = shard_rows(height, row_offset, row_stride);
     const size_t npix = (size_t)rows * width;
-    int rc = ensure_buf(c, c->rng, npix * 6 * sizeof(unsigned));
+    int rc = quiesce(c);  // a render on a caller's stream may still use the state
+    if (!rc) rc = ensure_buf(c, c->rng, npix * 6 * sizeof(unsigned));
     if (!rc) rc = ensure_buf(c, c->accum, npix * 3 * sizeof(float));
     if (rc) return rc;
     HIP_TRY(c, hipMemsetAsync(c->accum.p, 0, npix * 3 * sizeof(float), c->stream));
@@ -929,6 +959,9 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.order_n = c->order_n;
         K.order_cap = (long)(c->gorder.bytes / sizeof(int));
     }
+    // renders continue each other's RNG / frameSum state: a launch on a
+    // different stream than the previous one waits for it (no host sync)
+    if (c->render_stream && c->render_stream != s) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_render, 0));
     rt_order_groups_last = 0;
     HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, s);
@@ -955,6 +988,8 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     }
     if (e != hipSuccess) return hip_fail(c, e, "rt_render_kernel launch");
     HIP_TRY(c, hipEventRecord(c->ev1, s));
+    HIP_TRY(c, hipEventRecord(c->ev_render, s));
+    c->render_stream = s;
     c->timed = true;
     c->last_stream = s;
     c->frame = first + (unsigned)samples;  // Main.cu:480 accumulatedFrames++
@@ -1010,6 +1045,16 @@ int rt_render_multi(rt_context* const* ctxs, int n, int width, int height, int s
             if (ctxs[j] == ctxs[i]) return fail(ctxs[i], RT_ERR_INVALID_ARGUMENT, "context listed twice");
     }
     const int active = n < height ? n : height;  // contexts beyond the image height get no rows
+    // a failure at context i leaves contexts 0..i-1 with renders and copies
+    // into their pinned buffers in flight: drain them before returning, so a
+    // later call cannot reuse host_rgba under a running copy
+    auto drain = [&](int launched, int rc) {
+        for (int j = 0; j < launched; j++) {
+            (void)hipSetDevice(ctxs[j]->device);
+            (void)hipStreamSynchronize(ctxs[j]->stream);
+        }
+        return rc;
+    };
     for (int i = 0; i < active; i++) {
         rt_context* c = ctxs[i];
         rt_render_params p;
@@ -1023,21 +1068,26 @@ int rt_render_multi(rt_context* const* ctxs, int n, int width, int height, int s
         rt_kparams K;
         unsigned first = 0;
         int rc = prepare(c, &p, K, first);
-        if (rc) return rc;
+        if (rc) return drain(i, rc);
         const size_t bytes = (size_t)c->rows * width * 4;
         rc = ensure_buf(c, c->rgba, bytes);
-        if (rc) return rc;
+        if (rc) return drain(i, rc);
         if (c->host_rgba_bytes < bytes) {
+            rc = quiesce(c);
+            if (rc) return drain(i, rc);
+            if (hipStreamSynchronize(c->stream) != hipSuccess) return drain(i, fail(c, RT_ERR_HIP, "stream sync"));
             if (c->host_rgba) (void)hipHostFree(c->host_rgba);
             c->host_rgba = nullptr;
             c->host_rgba_bytes = 0;
-            HIP_TRY(c, hipHostMalloc(&c->host_rgba, bytes, hipHostMallocDefault));
+            const hipError_t e = hipHostMalloc(&c->host_rgba, bytes, hipHostMallocDefault);
+            if (e != hipSuccess) return drain(i, hip_fail(c, e, "hipHostMalloc"));
             c->host_rgba_bytes = bytes;
         }
         K.rgba = (unsigned*)c->rgba.p;
         rc = launch(c, K, c->stream, first, samples);
-        if (rc) return rc;
-        HIP_TRY(c, hipMemcpyAsync(c->host_rgba, c->rgba.p, bytes, hipMemcpyDeviceToHost, c->stream));
+        if (rc) return drain(i + 1, rc);
+        const hipError_t e = hipMemcpyAsync(c->host_rgba, c->rgba.p, bytes, hipMemcpyDeviceToHost, c->stream);
+        if (e != hipSuccess) return drain(i + 1, hip_fail(c, e, "hipMemcpyAsync"));
     }
     for (int i = 0; i < active; i++) {
         rt_context* c = ctxs[i];
@@ -1114,15 +1164,20 @@ int rt_set_state(rt_context* c, const uint32_t* rng, const float* accum, unsigne
     if (!c->rng.p) return fail(c, RT_ERR_INVALID_ARGUMENT, "no shard state (rt_init_rand first)");
     if (frame_counter == 0) return fail(c, RT_ERR_INVALID_ARGUMENT, "frame_counter must be >= 1");
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const int rc = quiesce(c);  // a render on a caller's stream may still use the state
+    if (rc) return rc;
     const size_t npix = (size_t)c->rows * c->width;
-    if (rng) HIP_TRY(c, hipMemcpy(c->rng.p, rng, npix * 6 * sizeof(unsigned), hipMemcpyHostToDevice));
+    std::vector<float> planes;
+    if (rng)
+        HIP_TRY(c, hipMemcpyAsync(c->rng.p, rng, npix * 6 * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
     if (accum) {
-        std::vector<float> planes(npix * 3);
+        planes.resize(npix * 3);
         for (size_t i = 0; i < npix; i++)
             for (int ch = 0; ch < 3; ch++) planes[ch * npix + i] = accum[3 * i + ch];
-        HIP_TRY(c, hipMemcpy(c->accum.p, planes.data(), npix * 3 * sizeof(float), hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemcpyAsync(c->accum.p, planes.data(), npix * 3 * sizeof(float), hipMemcpyHostToDevice,
+                                  c->stream));
     }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->frame = frame_counter;
     return RT_OK;
 }

@@ -1082,10 +1082,12 @@ rt_render_sorted_kernel(rt_kparams K) {
     int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
     float* rec_k = rec_base + LL * BLOCK + tid;
     float* rec_c = rec_base + 2 * LL * BLOCK + tid;
+    // global levels LL .. levels-1 only: plane (l - LL) of each field
+    const int GL = levels - LL;
     float* grec_mem = GREC ? K.rec + (long)blockIdx.x * BLOCK : rec_base;
     int* grec_code = reinterpret_cast<int*>(grec_mem) + tid;
-    float* grec_k = grec_mem + levels * RS + tid;
-    float* grec_c = grec_mem + 2 * levels * RS + tid;
+    float* grec_k = grec_mem + GL * RS + tid;
+    float* grec_c = grec_mem + 2 * GL * RS + tid;
     float* slots = rec_base + 3 * LL * BLOCK;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
     // counters[0..3]: queue fronts/backs (2 parities)
@@ -1128,7 +1130,8 @@ rt_render_sorted_kernel(rt_kparams K) {
         const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
         if (GREC)
             for (int l = nrec - 1; l >= LL; --l)
-                fold_level(grec_code[l * RS], grec_k[l * RS], grec_c[l * RS], hit_tab, lx, ly, lz);
+                fold_level(grec_code[(l - LL) * RS], grec_k[(l - LL) * RS], grec_c[(l - LL) * RS], hit_tab, lx, ly,
+                           lz);
         fold_records(rec_code, rec_k, rec_c, BLOCK, nrec < LL ? nrec : LL, hit_tab, lx, ly, lz);
         if (px.frame == 1u) {
             px.ax = 0.0f;
@@ -1325,9 +1328,9 @@ rt_render_sorted_kernel(rt_kparams K) {
                         rec_k[depth * BLOCK] = kspec;
                         rec_c[depth * BLOCK] = cosang;
                     } else {
-                        grec_code[depth * RS] = code;
-                        grec_k[depth * RS] = kspec;
-                        grec_c[depth * RS] = cosang;
+                        grec_code[(depth - LL) * RS] = code;
+                        grec_k[(depth - LL) * RS] = kspec;
+                        grec_c[(depth - LL) * RS] = cosang;
                     }
                     o = hP;
                     d = r;
@@ -1745,16 +1748,20 @@ bool rt_render_wants_global_records(const rt_kparams& K) {
     return groups < RT_WAVES_PER_EU;
 }
 
-// Floats of a global-memory record stack for one launch: 3 * max_bounces
-// planes over the grid's lanes (the grid covers every work item, rounded up
-// to the largest workgroup).
+// Floats of a global-memory record stack for one launch: 3 planes per level
+// kept in global memory (levels RT_GREC_LDS_LEVELS .. max_bounces-1; the
+// shallow ones stay in LDS) over the grid's lanes (the grid covers every work
+// item, rounded up to the largest workgroup).  At least one float, so a
+// forced global-record launch with no global level still gets a buffer.
 size_t rt_render_rec_floats(const rt_kparams& K) {
     long nitems = (long)K.rows * K.width;
     if (K.tile_w > 0) {
         const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
         nitems = tiles_x * tiles_y * 64;
     }
-    return (size_t)3 * K.max_bounces * (size_t)((nitems + 255) / 256 * 256);
+    const int lds_levels = K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS;
+    const size_t planes = (size_t)3 * (K.max_bounces - lds_levels);
+    return planes ? planes * (size_t)((nitems + 255) / 256 * 256) : 1;
 }
 
 // LDS bytes of one workgroup: hit table (if staged) + 3 record dwords per

@@ -81,8 +81,9 @@ struct rt_kparams {
     // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
     float cull_omax;
     // recursion record stack in global memory (sorted kernel, deep paths):
-    // 3 * max_bounces planes of rec_stride floats ([field][level][lane]);
-    // null = records in LDS
+    // levels 0 .. RT_GREC_LDS_LEVELS-1 stay in LDS, the deeper ones take
+    // 3 * (max_bounces - RT_GREC_LDS_LEVELS) planes of rec_stride floats
+    // ([field][level - RT_GREC_LDS_LEVELS][lane]); null = all records in LDS
     float* rec;
     int rec_stride;             // lanes in the grid (set by the launcher)
     // launch-order feedback (sorted kernel): workgroup g renders tile-group

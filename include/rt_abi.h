@@ -165,7 +165,10 @@ RT_API int rt_create(int device, rt_context** out);
 RT_API void rt_destroy(rt_context* ctx);
 
 /* Upload a copy of the scene (≈ allocateScene, Main.cu:38-109).  Resets the
- * frame counter to 1, like any camera change in controls(). */
+ * frame counter to 1, like any camera change in controls().  Waits for a
+ * render still running on a caller's stream (rt_render_device) first; so do
+ * rt_init_rand and rt_set_state.  Scenes with 2^24 or more spheres +
+ * triangles + quads in the BVH return RT_ERR_UNSUPPORTED. */
 RT_API int rt_set_scene(rt_context* ctx, const rt_scene* scene);
 
 /* Move the camera (controls(), Controls.cuh:5-75): resets accumulation. */
@@ -241,7 +244,9 @@ RT_API int rt_render_ex(rt_context* ctx, const rt_render_params* p,
 
 /* Asynchronous render into DEVICE memory (rows*width*4 bytes, 4-byte
  * aligned) on HIP stream `stream` (hipStream_t; NULL = the context's own
- * stream).  Returns after the launch; the frame counter advances. */
+ * stream).  Returns after the launch; the frame counter advances.  A render
+ * on a different stream than the context's previous render is ordered after
+ * it on the device (stream wait on an event; no host synchronisation). */
 RT_API int rt_render_device(rt_context* ctx, const rt_render_params* p,
                             void* rgba_device, void* stream);
 
@@ -256,7 +261,10 @@ RT_API int rt_synchronize(rt_context* ctx);
  * streams; the RGBA8 rows are gathered into rgba_out (host, width*height*4,
  * row 0 = bottom; may be NULL).  Keep the contexts' frame counters in step by
  * always rendering them together.  Equal to one context rendering the whole
- * image (tests/test_gpu_parity.py). */
+ * image (tests/test_gpu_parity.py).  On failure every context's queued work
+ * has finished when the call returns, but the contexts that did launch have
+ * advanced their RNG state and frame counter while the others have not:
+ * re-seed all of them (rt_init_rand) before rendering together again. */
 RT_API int rt_render_multi(rt_context* const* ctxs, int n, int width, int height, int samples,
                            uint8_t* rgba_out);
 

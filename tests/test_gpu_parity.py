@@ -330,6 +330,49 @@ def test_render_device_into_torch_buffer(gpu, oracle):
     assert gpu.last_kernel_ms() > 0
 
 
+def test_state_writes_wait_for_device_render(gpu, oracle):
+    """rt_set_scene / rt_init_rand / rt_set_state right after an asynchronous
+    rt_render_device on a torch stream must not overwrite the scene or the
+    shard state under the running kernel (they wait for that stream), and a
+    render on the context's own stream after one on a torch stream continues
+    its state in order."""
+    import torch
+    w, h, spp, mb = 640, 360, 8, 4
+    s07, s04 = scenes.scene_07(), scenes.scene_04()
+    stream = torch.cuda.Stream()
+    buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    seeds = oracle.OracleState(w, h)
+    oracle.render(s07, seeds, 0, mb, first_frame=1)  # curand_init states only
+    st = oracle.OracleState(w, h)
+    oracle.render(s07, st, spp, mb, first_frame=1)
+    for _ in range(3):
+        # scene swap queued behind the render
+        gpu.set_scene(s07)
+        gpu.init_rand(w, h)
+        gpu.render_device(gpu.params(w, h, spp, mb, first_frame=1), buf.data_ptr(), stream.cuda_stream)
+        gpu.set_scene(s04)
+        stream.synchronize()
+        assert np.array_equal(buf.cpu().numpy().view(np.uint8).reshape(h, w, 4), st.rgba)
+        # reseed queued behind the render: the fresh seeds must survive it
+        gpu.set_scene(s07)
+        gpu.render_device(gpu.params(w, h, spp, mb, first_frame=1), buf.data_ptr(), stream.cuda_stream)
+        gpu.init_rand(w, h)
+        rng, _ = gpu.get_state(h, w)
+        assert np.array_equal(rng, seeds.rng)
+        # checkpoint restore queued behind the render
+        gpu.render_device(gpu.params(w, h, spp, mb, first_frame=1), buf.data_ptr(), stream.cuda_stream)
+        gpu.set_state(seeds.rng, np.zeros((h, w, 3), np.float32), 1)
+        rng, _ = gpu.get_state(h, w)
+        assert np.array_equal(rng, seeds.rng)
+    # device render on a torch stream, then a synchronous continuation on
+    # the context's stream: frames 1..4 then 5..8 equal one 8-frame render
+    gpu.init_rand(w, h)
+    gpu.render_device(gpu.params(w, h, 4, mb, first_frame=1), buf.data_ptr(), stream.cuda_stream)
+    img = gpu.render(w, h, 4, mb)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
 def test_cli_progressive_loop_with_controls(bwrt_lib, oracle, tmp_path):
     """The C++ host loop (host/bwrt_render.cpp, Main.cu:467-496): 2 frames,
     then W+LEFT held for one frame (controls() restarts accumulation), then 4
@@ -502,11 +545,13 @@ def _fresh_renderer(bwrt_lib, monkeypatch, **env):
 
 
 @pytest.mark.parametrize("block", [64, 128, 256])
-@pytest.mark.parametrize("w,h,mb", [(160, 90, 4), (100, 37, 6)])
+@pytest.mark.parametrize("w,h,mb", [(160, 90, 4), (100, 37, 6), (160, 90, 2), (120, 70, 3), (64, 40, 0)])
 def test_global_records_forced(bwrt_lib, oracle, monkeypatch, block, w, h, mb):
     """The sorted kernel with its recursion records in global memory
     (BWRT_GREC=1; the launch policy picks it for deep paths such as config 4)
-    at every workgroup size, including ragged sizes and a row shard."""
+    at every workgroup size, including ragged sizes and a row shard.  Levels
+    0-1 stay in LDS: at max_bounces 2 no level reaches global memory, at 3
+    exactly one does (the boundaries of the split)."""
     r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_GREC=1, BWRT_BLOCK=block)
     try:
         for off, stride in ((0, 1), (1, 3)):
@@ -547,17 +592,21 @@ def test_bvh_through_sorted_kernel(bwrt_lib, oracle, monkeypatch, name):
         r.close()
 
 
-@pytest.mark.parametrize("scene_name,w,h,spp,mb", [("07", 1920, 1080, 2, 4), ("04", 1600, 1200, 2, 3)])
-def test_launch_order_feedback(bwrt_lib, oracle, monkeypatch, scene_name, w, h, spp, mb):
+@pytest.mark.parametrize("scene_name,w,h,spp,mb,grec", [("07", 1920, 1080, 2, 4, 0), ("04", 1600, 1200, 2, 3, 0),
+                                                       ("07", 1920, 1080, 2, 6, 1)])
+def test_launch_order_feedback(bwrt_lib, oracle, monkeypatch, scene_name, w, h, spp, mb, grec):
     """Launch-order feedback (grids of several resident generations: each
     launch records its tile-groups' durations and the next launch starts the
     most expensive first): the first render runs in blockIdx order, the
     following ones reordered — every one equals the oracle bit for bit, and
-    a progressive continuation under the new order does too."""
+    a progressive continuation under the new order does too.  The grec case
+    is config 4's product path (maxBounces 6: global-memory records, levels
+    2-5 outside LDS) reordered."""
     scene = scenes.SCENES[scene_name]()
     st = oracle.OracleState(w, h)
     oracle.render(scene, st, spp, mb, first_frame=1)
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1, BWRT_GREC=grec) if grec else \
+        _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
     try:
         r.set_scene(scene)
         for _ in range(3):
