@@ -93,6 +93,9 @@ struct rt_context {
     int bvh_order_mask = 7;
     DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table | bvh nodes | bvh prims
     size_t off_bvh = 0, off_bvh_prims = 0;  // in floats; 0 = no BVH
+    size_t off_bvh16 = 0;                   // 16-byte nodes (0 = none: boxes beyond fp16)
+    float ovf_sc = 0.0f, ovf_nm = 0.0f, ovf_im = 0.0f;  // overflow bounds (rt_layout.h)
+    float cull_dmax = -1.0f;                            // culled rays: max|d_i| bound
     size_t off_pln = 0, off_tri = 0, off_quad = 0, off_hit = 0;  // in floats
 
     // shard state
@@ -301,12 +304,38 @@ struct BvhBuilder {
     static constexpr int kBins = 16;
     int max_leaf = 8;         // BWRT_BVH_LEAF
     float trav_cost = 0.0f;   // BWRT_BVH_CT: SAH cost of one node step relative to one primitive test
-    int order_mask = 7;       // BWRT_BVH_ORDER_MASK: octant bits that get their own node array
+    int order_mask = 7;       // octant bits that get their own node array (set from the scene extents; BWRT_BVH_ORDER_MASK)
     std::vector<BvhItem> items;
     std::vector<BvhNode> tree;
     std::vector<int> prims;
-    std::vector<float> nodes;  // 6 orders x n_nodes x 8 floats
+    std::vector<float> nodes;  // 8 orders x n_nodes x 8 floats
+    // the same threaded arrays as 16-byte nodes (rt_layout.h bvh_nodes16):
+    // boxes in fp16 rounded outward; n16 = every box fits the fp16 range
+    std::vector<uint32_t> nodes16;  // 8 orders x n_nodes x 4 words
+    bool n16 = false;
     int n_nodes = 0;
+
+    // fp16 bits of the largest half <= v (down) or the smallest half >= v
+    // (up); false if |v| exceeds the finite fp16 range
+    static bool half_bound(float v, bool up, uint16_t& out) {
+        if (!(std::fabs(v) <= 65504.0f)) return false;
+        if (std::fabs(v) < 6.103515625e-05f) {  // below the smallest normal: +-2^-14
+            out = up ? 0x0400 : 0x8400;
+            return true;
+        }
+        uint32_t f;
+        std::memcpy(&f, &v, 4);
+        const uint32_t sign = (f >> 16) & 0x8000u;
+        const int e = (int)((f >> 23) & 0xff) - 127 + 15;  // 1..30 here
+        uint32_t m = (f >> 13) & 0x3ffu;                   // truncated toward zero
+        uint16_t h = (uint16_t)(sign | ((uint32_t)e << 10) | m);
+        const bool inexact = (f & 0x1fffu) != 0;
+        // truncation moved |v| down: step one ulp outward when that is the wrong way
+        if (inexact && (up != (sign != 0))) h = (uint16_t)(h + 1);  // away from zero
+        if (((h >> 10) & 0x1f) == 0x1f) return false;             // stepped to infinity
+        out = h;
+        return true;
+    }
 
     static float inflate(float v) { return 1e-3f + 1e-4f * std::fabs(v); }
     static float area(const float* lo, const float* hi) {
@@ -432,6 +461,8 @@ struct BvhBuilder {
     void finish() {
         n_nodes = (int)tree.size();
         nodes.assign((size_t)8 * n_nodes * 8, 0.0f);
+        nodes16.assign((size_t)8 * n_nodes * 4, 0u);
+        n16 = true;
         std::vector<int> pos(n_nodes), seq, end(n_nodes);
         for (int order = 0; order < 8; order++) {
             if (order & ~order_mask) continue;  // never selected by the kernel
@@ -454,6 +485,19 @@ struct BvhBuilder {
                 const int leaf = t.left < 0 ? ((t.count << 24) | t.first) : -1;
                 std::memcpy(&nd[3], &miss, 4);
                 std::memcpy(&nd[7], &leaf, 4);
+                // 16-byte node: {lo.x | lo.y, lo.z | hi.x, hi.y | hi.z} in fp16
+                // (lo rounded down, hi up) + w: the miss link of an internal node
+                // (-1 = done) or ~leaf of a leaf (count >= 1, so w < -2^24; a
+                // leaf's miss link is always the next node, i + 1)
+                uint16_t hb[6];
+                for (int a = 0; a < 3; a++)
+                    n16 = n16 && half_bound(t.lo[a], false, hb[a]) && half_bound(t.hi[a], true, hb[3 + a]);
+                uint32_t* q = nodes16.data() + ((size_t)order * n_nodes + i) * 4;
+                q[0] = hb[0] | (uint32_t)hb[1] << 16;
+                q[1] = hb[2] | (uint32_t)hb[3] << 16;
+                q[2] = hb[4] | (uint32_t)hb[5] << 16;
+                const int w = t.left < 0 ? ~leaf : miss;
+                std::memcpy(&q[3], &w, 4);
             }
         }
     }
@@ -611,8 +655,60 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     for (int i = 0; i < nq; i++, id++)
         compile_polygon(h.data() + off_quad + (size_t)i * RT_QUAD_FLOATS, hit + (size_t)id * RT_HIT_FLOATS,
                         s->quads[i].vertices, 4, s->quads[i].mat, scale);
+    // overflow bounds of the bounded primitives' tests (rt_layout.h ovf_*;
+    // a NaN or inf input makes its bound infinite, so no ray is culled and
+    // every BVH ray takes the brute-force loop)
+    {
+        double sc = 0.0, rmax = 0.0, nm = 0.0, im = 0.0;
+        auto upd = [](double& b, float x) {
+            const double a = std::fabs((double)x);
+            if (!(a <= b)) b = std::isnan(a) ? INFINITY : a;
+        };
+        for (int i = 0; i < ns; i++) {
+            const rt_sphere& sp = s->spheres[i];
+            upd(sc, sp.position.x);
+            upd(sc, sp.position.y);
+            upd(sc, sp.position.z);
+            upd(rmax, sp.radius);
+        }
+        auto polyb = [&](const rt_vec3* v, int nv, const float* rec) {
+            for (int k = 0; k < nv; k++) {
+                upd(sc, v[k].x);
+                upd(sc, v[k].y);
+                upd(sc, v[k].z);
+            }
+            for (int a = 0; a < 3; a++) upd(nm, rec[a]);
+            for (int k = 0; k < nv; k++)  // {v_k[3], in_k[3]} from float 4 on
+                for (int a = 0; a < 3; a++) upd(im, rec[4 + 6 * k + 3 + a]);
+        };
+        for (int i = 0; i < nt; i++) polyb(s->triangles[i].vertices, 3, h.data() + off_tri + (size_t)i * RT_TRI_FLOATS);
+        for (int i = 0; i < nq; i++) polyb(s->quads[i].vertices, 4, h.data() + off_quad + (size_t)i * RT_QUAD_FLOATS);
+        const double S = (sc + rmax) * (1.0 + 1e-6), N = nm * (1.0 + 1e-6), I = im * (1.0 + 1e-6);
+        c->ovf_sc = (float)std::min(S, 3e38);
+        c->ovf_nm = (float)std::min(N, 3e38);
+        c->ovf_im = (float)std::min(I, 3e38);
+        // culling (polygon_test) skips only polygons whose exact test rejects
+        // the ray; a NaN in the inside test would instead accept it, so rays
+        // are culled only when, for every origin within cull_omax, no polygon
+        // test can overflow: max|d_i| <= cull_dmax (the bounds of the
+        // kernel's bvh_safe with om = cull_omax, halved)
+        double dmax = INFINITY;
+        if (c->cull_omax > 0.0f) {
+            const double om = c->cull_omax;
+            dmax = std::min(dmax, 1e18 / (om + S));
+            if (N > 0.0) {
+                dmax = std::min(dmax, 1e36 / N);
+                dmax = std::min(dmax, (1e37 - om - S) / (6e4 * N * (om + 3.0 * S)));  // P finite
+                if (I > 0.0) dmax = std::min(dmax, (3e36 / I - om - S) / (6e4 * N * (om + 3.0 * S)));
+                if (!(N * (om + 3.0 * S) < 1e33)) dmax = -1.0;  // t = num / nd may overflow
+            }
+            dmax *= 0.5;
+        }
+        c->cull_dmax = std::isfinite(dmax) ? (float)std::min(dmax, 3e38) : (dmax > 0.0 ? INFINITY : -1.0f);
+        if (!(c->cull_dmax > 0.0f)) c->cull_dmax = -1.0f;
+    }
     // BVH for large scenes (BWRT_BVH_MIN primitives, default 64)
-    size_t off_bvh = 0, off_bvh_prims = 0;
+    size_t off_bvh = 0, off_bvh_prims = 0, off_bvh16 = 0;
     {
         int bvh_min = 64;
         if (const char* e = std::getenv("BWRT_BVH_MIN")) bvh_min = std::atoi(e);
@@ -648,15 +744,37 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             // bit clear (a negative value means "internal node" to the kernels)
             if (const char* e = std::getenv("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 127);
             if (const char* e = std::getenv("BWRT_BVH_CT")) B.trav_cost = (float)std::atof(e);
-            if (const char* e = std::getenv("BWRT_BVH_ORDER_MASK")) B.order_mask = std::atoi(e) & 7;
             B.build(0, nb);
+            // octant arrays only along the scene's long axes (extent >= half
+            // the longest): each bit doubles the node data the walks spread
+            // over the caches, and a short axis buys little front-to-back
+            // order.  Config 5 (extents ~25 / 9 / 31): x and z, 157 -> 147 ms
+            // with 16-byte nodes (all three axes; z alone 187, x alone 272)
+            {
+                const BvhNode& root = B.tree[0];
+                float ext[3], mx = 0.0f;
+                for (int a = 0; a < 3; a++) mx = std::max(mx, ext[a] = root.hi[a] - root.lo[a]);
+                B.order_mask = 0;
+                for (int a = 0; a < 3; a++)
+                    if (!(ext[a] < 0.5f * mx)) B.order_mask |= 1 << a;
+            }
+            if (const char* e = std::getenv("BWRT_BVH_ORDER_MASK")) B.order_mask = std::atoi(e) & 7;
             B.finish();
+            if (std::getenv("BWRT_BVH_STATS")) {  // diagnostics (tests, tuning)
+                long ax[3] = {0, 0, 0}, inner = 0;
+                for (const BvhNode& t : B.tree)
+                    if (t.left >= 0) ax[t.axis]++, inner++;
+                std::fprintf(stderr, "bvh: %d nodes, %ld internal, split axes x %ld y %ld z %ld, octant mask %d, n16 %d\n",
+                             (int)B.tree.size(), inner, ax[0], ax[1], ax[2], B.order_mask, B.n16 ? 1 : 0);
+            }
             c->bvh_nodes_per_order = B.n_nodes;
             c->bvh_order_mask = B.order_mask;
             off_bvh = (total + 3) & ~(size_t)3;
             off_bvh_prims = off_bvh + B.nodes.size();  // leaf records, RT_LEAF_FLOATS each
-            h.resize(off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS + 4, 0.0f);
+            off_bvh16 = B.n16 ? off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS : 0;
+            h.resize(off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS + (B.n16 ? B.nodes16.size() : 0) + 4, 0.0f);
             std::memcpy(h.data() + off_bvh, B.nodes.data(), B.nodes.size() * sizeof(float));
+            if (B.n16) std::memcpy(h.data() + off_bvh16, B.nodes16.data(), B.nodes16.size() * sizeof(uint32_t));
             for (size_t j = 0; j < B.prims.size(); j++) {
                 const int id = B.prims[j];
                 float* r = h.data() + off_bvh_prims + j * RT_LEAF_FLOATS;
@@ -695,6 +813,7 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     c->off_hit = off_hit;
     c->off_bvh = off_bvh;
     c->off_bvh_prims = off_bvh_prims;
+    c->off_bvh16 = std::getenv("BWRT_BVH_N16") && !std::atoi(std::getenv("BWRT_BVH_N16")) ? 0 : off_bvh16;
     c->camera = s->camera;
     c->has_scene = true;
     c->frame = 1;
@@ -911,6 +1030,12 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.hit = base + c->off_hit;
     K.bvh_nodes = c->off_bvh ? base + c->off_bvh : nullptr;
     K.bvh_leafrec = c->off_bvh ? base + c->off_bvh_prims : nullptr;
+    K.bvh_nodes16 = c->off_bvh && c->off_bvh16 ? reinterpret_cast<const unsigned*>(base + c->off_bvh16) : nullptr;
+    K.bvh_n_nodes = c->bvh_nodes_per_order;
+    K.ovf_sc = c->ovf_sc;
+    K.ovf_nm = c->ovf_nm;
+    K.ovf_im = c->ovf_im;
+    K.cull_dmax = c->cull_dmax;
     K.rng = (unsigned*)c->rng.p;
     K.accum = (float*)c->accum.p;
     return RT_OK;

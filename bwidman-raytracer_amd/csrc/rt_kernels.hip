@@ -279,14 +279,15 @@ __device__ __forceinline__ bool polygon_edges(const __attribute__((address_space
 
 struct CullRay {
     float a, a_k;  // |d|^2, |d|^2 (1 - 2^-14)
-    bool ok;       // max|o_i| <= K.cull_omax
+    bool ok;       // max|o_i| <= K.cull_omax and max|d_i| <= K.cull_dmax
 };
 
-__device__ __forceinline__ CullRay cull_ray(const rt_kparams& K, f3 o, float a) {
+__device__ __forceinline__ CullRay cull_ray(const rt_kparams& K, f3 o, f3 d, float a) {
     CullRay c;
     c.a = a;
     c.a_k = a * (1.0f - 6.103515625e-05f);
-    c.ok = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= K.cull_omax;
+    c.ok = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= K.cull_omax &&
+           fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z)) <= K.cull_dmax;
     return c;
 }
 
@@ -338,7 +339,7 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
     const int pln_base = K.n_sph;
     const int tri_base = K.n_sph + K.n_pln;
     const int quad_base = tri_base + K.n_tri;
-    const CullRay cr = cull_ray(K, o, a);
+    const CullRay cr = cull_ray(K, o, d, a);
     RT_BRANCH_COUNT(K, 4);
     for (int i = 0; i < K.n_max; i++) {
         if (i < K.n_sph) {  // Intersection.cuh:15-62
@@ -383,13 +384,47 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
 // so the winner is the minimum distance with ties resolved to the primitive
 // the reference tests last (RT_KEY order) — exactly what the reference's
 // running `t > closest` test in interleaved order returns, whatever order
-// the BVH visits primitives in.  This needs finite rays (all t finite, never
-// NaN); a ray with a NaN/inf component takes the brute-force loop, which
-// reproduces the reference's NaN acceptance behaviour.  Node boxes are
-// inflated far beyond float rounding and the slab test only ever prunes
-// with margins, so no primitive the reference could hit is skipped.
+// the BVH visits primitives in.  This needs distances that are never NaN:
+// the reference ACCEPTS a NaN distance (its `t <= nearZero || t > closest`
+// rejection is false for NaN) and then every later candidate, which only its
+// own loop order reproduces.  Rays with a NaN/inf component, and finite rays
+// whose primitive tests could overflow to NaN (bvh_safe), take the
+// brute-force loop.  Node boxes are inflated far beyond float rounding and
+// the slab test only ever prunes with margins, so no primitive the
+// reference could hit is skipped.
 __device__ __forceinline__ bool key_accept(float t, int key, float best_t, int best_key) {
     return !(t <= RT_NEAR_ZERO) && (t < best_t || (t == best_t && key > best_key));
+}
+
+// No bounded-primitive test of this ray can produce a NaN distance: with
+// dm = max|d_i|, om = max|o_i|, S = K.ovf_sc (largest vertex / sphere
+// centre coordinate + sphere radius), N = K.ovf_nm (largest component of
+// a compiled triangle/quad normal cross(e0, e1), |n| = 2 area) and
+// K.ovf_im (largest component of an inner edge normal cross(n, e_k)), the sphere
+// test's b^2 and 4ac stay below 36 (dm (om + S))^2 < FLT_MAX and the polygon
+// plane's n.d and n.o + d below 3 N dm and 3 N (om + 3 S): no inf - inf, no
+// inf / inf.  Secondary rays are not unit vectors (the reference reflects
+// about un-normalised triangle normals, Main.cu:187-191, Intersection.cuh:
+// 108-138), so at scene scales >= 100 their direction reaches 1e16 and
+// overflow does happen (tests/test_gpu_parity.py test_stress_bvh_scaled).
+// Infinite distances need no special care: the reference and key_accept
+// both keep the last of equal distances, and a box is only pruned against
+// a finite closest hit.
+__device__ __forceinline__ bool bvh_safe(const rt_kparams& K, f3 o, f3 d) {
+    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float dm = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    // (NaN components fail every comparison, inf ones the first; dm > 1e-15
+    // keeps a = |d|^2 normal, so a2 > 0 and (-b - sqrt(disc)) / a2 is never 0/0)
+    // The polygon inside test dot(in_k, P - v_k) must not overflow either (a
+    // NaN there passes it, so the reference accepts a hit anywhere on the
+    // polygon's plane): P = o + t d with t <= |n.o + d| / 1e-4 (|n.d| >= 1e-4
+    // or the plane is rejected), so |P - v_k| <= om + S + 1.8 dm 3e4 N (om + 3S)
+    // and |in_k| <= K.ovf_im per component
+    if (!(om + K.ovf_sc < 1e18f && dm < 1e18f && dm > 1e-15f && dm * (om + K.ovf_sc) < 1e18f &&
+          K.ovf_nm * dm < 1e36f && K.ovf_nm * (om + 3.0f * K.ovf_sc) < 1e33f))
+        return false;
+    const float pm = om + K.ovf_sc + 6e4f * dm * (K.ovf_nm * (om + 3.0f * K.ovf_sc));
+    return pm < 1e37f && K.ovf_im * pm < 3e36f;
 }
 
 // Leaf record (rt_layout.h RT_LEAF_FLOATS): {id, key, kind, 0, record...};
@@ -491,9 +526,7 @@ __device__ __forceinline__ void prim_test(const rt_kparams& K, int id, f3 o, f3 
 }
 
 __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
-    const bool finite = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
-                        fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
-    if (!finite) {  // NaN/inf rays: the reference's interleaved loop
+    if (!bvh_safe(K, o, d)) {  // NaN/inf rays, overflowing tests: the reference's interleaved loop
         closest_hit_brute(K, o, d, best_t, best_id);
         return;
     }
@@ -1423,7 +1456,14 @@ rt_render_sorted_kernel(rt_kparams K) {
 #ifndef RT_REFILL
 #define RT_REFILL 40
 #endif
-template <int BLOCK>
+// fp16 bits -> float (exact)
+__device__ __forceinline__ float h2f(unsigned bits) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(bits & 0xffffu));
+}
+
+// N16: 16-byte nodes (rt_layout.h bvh_nodes16) — one gather per node visit
+// instead of two; the walk, its tests and its order are the same
+template <int BLOCK, bool N16>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
 rt_render_bvh_refill_kernel(rt_kparams K) {
     extern __shared__ float smem[];
@@ -1451,12 +1491,34 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     f3 inv = o, oinv = o;
     float m = 0.0f, a2 = 0.0f, a4 = 0.0f;
     const float* nodes = K.bvh_nodes;
+    const unsigned* nodes16 = K.bvh_nodes16;
+    const int nn = K.bvh_n_nodes;
 
     while (true) {
         // (A) lanes without a walk: shade the finished query, start the next ray
         while (!walking && !idle) {
             if (pending) {
                 pending = false;
+#ifdef RT_BVH_CHECK
+                // diagnostic build: the brute-force loop on the same ray; a
+                // disagreement is logged to K.stamps (BWRT_GTIMES buffer):
+                // [0] count, then 16 words per record
+                {
+                    float bt;
+                    int bi;
+                    closest_hit_brute(K, o, d, bt, bi);
+                    if ((bi != best_id || (bi >= 0 && bt != best_t && !(bt != bt && best_t != best_t))) && K.stamps) {
+                        const unsigned long long k = atomicAdd(&K.stamps[0], 1ull);
+                        if (k < 4096) {
+                            unsigned long long* rec = K.stamps + 16 + 16 * k;
+                            rec[0] = __float_as_uint(o.x); rec[1] = __float_as_uint(o.y); rec[2] = __float_as_uint(o.z);
+                            rec[3] = __float_as_uint(d.x); rec[4] = __float_as_uint(d.y); rec[5] = __float_as_uint(d.z);
+                            rec[6] = __float_as_uint(best_t); rec[7] = (unsigned)best_id;
+                            rec[8] = __float_as_uint(bt); rec[9] = (unsigned)bi; rec[10] = (unsigned)depth;
+                        }
+                    }
+                }
+#endif
                 bool finished = true;
                 if (best_id >= 0) {  // shade (Main.cu:237-264), as rt_render_kernel
                     const float* h = hit_tab + RT_HIT_FLOATS * best_id;
@@ -1519,9 +1581,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             best_t = INFINITY;
             best_id = -1;
             best_key = -1;
-            const bool finite = fabsf(o.x) < INFINITY && fabsf(o.y) < INFINITY && fabsf(o.z) < INFINITY &&
-                                fabsf(d.x) < INFINITY && fabsf(d.y) < INFINITY && fabsf(d.z) < INFINITY;
-            if (!finite) {  // NaN/inf rays: the reference's interleaved loop
+            if (!bvh_safe(K, o, d)) {  // NaN/inf rays, overflowing tests: the reference's interleaved loop
                 closest_hit_brute(K, o, d, best_t, best_id);
                 pending = true;
                 continue;
@@ -1549,7 +1609,10 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             oinv = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
             m = 1e-6f + 9.5367431640625e-07f * fmaxf(fmaxf(fabsf(oinv.x), fabsf(oinv.y)), fabsf(oinv.z));
             const int order = ((d.x < 0.0f) | ((d.y < 0.0f) << 1) | ((d.z < 0.0f) << 2)) & K.bvh_order_mask;
-            nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
+            if (N16)
+                nodes16 = K.bvh_nodes16 + (size_t)order * nn * 4;
+            else
+                nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
             node = 0;
             leaf = -1;
             walking = true;
@@ -1562,8 +1625,18 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 bool stalled = false;
                 if (walking && node >= 0) {
                     RT_BRANCH_COUNT(K, 5);
-                    const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
-                    const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
+                    float4 lo, hi;
+                    if (N16) {
+                        const uint4 q = *reinterpret_cast<const uint4*>(nodes16 + 4 * node);
+                        const int w = (int)q.w;
+                        const bool lnode = w < -1;  // a leaf: ~leaf, its miss link is the next node
+                        lo = make_float4(h2f(q.x), h2f(q.x >> 16), h2f(q.y),
+                                         __int_as_float(lnode ? (node + 1 < nn ? node + 1 : -1) : w));
+                        hi = make_float4(h2f(q.y >> 16), h2f(q.z), h2f(q.z >> 16), __int_as_float(lnode ? ~w : -1));
+                    } else {
+                        lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
+                        hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
+                    }
                     const float tx0 = __builtin_fmaf(lo.x, inv.x, -oinv.x), tx1 = __builtin_fmaf(hi.x, inv.x, -oinv.x);
                     const float ty0 = __builtin_fmaf(lo.y, inv.y, -oinv.y), ty1 = __builtin_fmaf(hi.y, inv.y, -oinv.y);
                     const float tz0 = __builtin_fmaf(lo.z, inv.z, -oinv.z), tz1 = __builtin_fmaf(hi.z, inv.z, -oinv.z);
@@ -1693,7 +1766,12 @@ hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, hipStream_t s) {
     }
     const long grid = (nitems + BLOCK - 1) / BLOCK;
     const size_t lds = (size_t)3 * (K.max_bounces + 1) * BLOCK * sizeof(float);
-    hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(BLOCK), lds, s, K);
+    if (K.bvh_nodes16)
+        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, true>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(BLOCK),
+                           lds, s, K);
+    else
+        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false>), dim3((unsigned)(grid < 1 ? 1 : grid)),
+                           dim3(BLOCK), lds, s, K);
     return hipGetLastError();
 }
 

@@ -77,9 +77,23 @@ struct rt_kparams {
     const float* bvh_leafrec;   // leaf records in leaf order, RT_LEAF_FLOATS each
     int bvh_order_stride;
     int bvh_order_mask;         // octant bits with their own arrays (7 = all three axes)
+    // the same arrays as 16-byte nodes (null when a box exceeds the fp16
+    // range), bvh_n_nodes x 4 words per octant: {lo.x | lo.y << 16,
+    // lo.z | hi.x << 16, hi.y | hi.z << 16} as fp16 rounded outward (lo down,
+    // hi up: the boxes only grow) and w = the miss link of an internal node
+    // (-1 = done) or ~leaf for a leaf, whose miss link is the next node
+    const unsigned* bvh_nodes16;
+    int bvh_n_nodes;
+    // overflow bounds of the bounded primitives' tests (kernel bvh_safe):
+    // largest |coordinate| of a vertex / sphere centre plus the largest
+    // radius, largest |component| of a triangle / quad normal cross(e0, e1)
+    // and of an inner edge normal cross(n, e_k)
+    float ovf_sc, ovf_nm, ovf_im;
     // conservative polygon culling (see polygon_test): only rays whose origin
-    // satisfies max|o_i| <= cull_omax may skip a polygon's exact test
+    // satisfies max|o_i| <= cull_omax and whose direction max|d_i| <=
+    // cull_dmax (no polygon test can overflow) may skip a polygon's exact test
     float cull_omax;
+    float cull_dmax;
     // recursion record stack in global memory (sorted kernel, deep paths):
     // levels 0 .. RT_GREC_LDS_LEVELS-1 stay in LDS, the deeper ones take
     // 3 * (max_bounces - RT_GREC_LDS_LEVELS) planes of rec_stride floats

@@ -77,12 +77,41 @@ def test_stress_scene_small(gpu, oracle):
     same_state(gpu, st)
 
 
-def test_stress_c5_rows_bvh(gpu, oracle):
+@pytest.mark.parametrize("n16,mask", [(None, None), ("0", None), (None, "7"), ("0", "7"), (None, "1")])
+def test_stress_c5_rows_bvh(gpu, oracle, monkeypatch, n16, mask):
     """Config-5 geometry (1920x1080 stress scene, 8 bounces) on 8 full-width
     rows (y = 3 mod 135): 10,256 primitives take the BVH path; the oracle is
     the reference's brute-force loop, so this pins the BVH's exact
-    key-ordered tie-breaking and conservative culling."""
+    key-ordered tie-breaking and conservative culling — with the default
+    16-byte fp16 nodes and octant arrays from the scene extents, with 32-byte
+    nodes (BWRT_BVH_N16=0) and with other octant masks."""
+    if n16 is not None:
+        monkeypatch.setenv("BWRT_BVH_N16", n16)
+    if mask is not None:
+        monkeypatch.setenv("BWRT_BVH_ORDER_MASK", mask)
     img, st = run_pair(gpu, oracle, scenes.stress_scene(), 1920, 1080, 2, 8, row_offset=3, row_stride=135)
+    monkeypatch.delenv("BWRT_BVH_N16", raising=False)
+    monkeypatch.delenv("BWRT_BVH_ORDER_MASK", raising=False)
+    gpu.set_scene(scenes.scene_07())
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+@pytest.mark.parametrize("k,n16,mb", [(3e4, 0, 6), (1e-4, 1, 6), (1.0, 1, 6), (100.0, 1, 1), (1e3, 1, 6), (1e10, 0, 3)])
+def test_stress_bvh_scaled(gpu, oracle, monkeypatch, capfd, k, n16, mb):
+    """The stress scene scaled by 3e4 (box corners beyond the fp16 range:
+    the BVH keeps 32-byte nodes) and by 1e-4 (corners down in the fp16
+    subnormal range, rounded out to +-2^-14).  From scale 100 up, secondary
+    directions reflected about the un-normalised triangle normals reach 1e16
+    and the reference's sphere test overflows to a NaN distance, which it
+    accepts: those rays must take the brute-force loop (bvh_safe).  At 1e10
+    every test overflows.  Bit-exact in every case."""
+    monkeypatch.setenv("BWRT_BVH_STATS", "1")
+    s = _scaled(scenes.stress_scene(), k)
+    img, st = run_pair(gpu, oracle, s, 96, 54, 2, mb)
+    monkeypatch.delenv("BWRT_BVH_STATS")
+    assert f"n16 {n16}" in capfd.readouterr().err
+    gpu.set_scene(scenes.scene_07())
     assert np.array_equal(img, st.rgba)
     same_state(gpu, st)
 
