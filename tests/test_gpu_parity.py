@@ -561,6 +561,24 @@ def test_random_scenes(gpu, oracle, monkeypatch, seed):
     same_state(gpu, st)
 
 
+@pytest.mark.parametrize("seed,k", [(3, 1e6), (5, 1e10), (7, 1e-6), (9, 1e-10), (11, 1e15), (13, 1e19)])
+@pytest.mark.parametrize("bvh", [False, True])
+def test_random_scenes_extreme_scales(gpu, oracle, monkeypatch, seed, k, bvh):
+    """Random scenes scaled far beyond any sensible range: overflow in the
+    reference's tests turns distances into inf / NaN, which the reference
+    accepts in its own way (a NaN distance is accepted, and then every later
+    candidate); the brute-force loop's culling and the BVH must step aside
+    for such rays (cull_dmax, bvh_safe) — bit-exact through both paths."""
+    if bvh:
+        monkeypatch.setenv("BWRT_BVH_MIN", "1")
+    s = _scaled(_random_scene(seed), k)
+    img, st = run_pair(gpu, oracle, s, 64, 36, 2, 4)
+    monkeypatch.delenv("BWRT_BVH_MIN", raising=False)
+    gpu.set_scene(scenes.scene_07())
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
 def _fresh_renderer(bwrt_lib, monkeypatch, **env):
     """A renderer created under BWRT_* launch knobs (read at rt_create)."""
     from bwrt import Renderer
