@@ -456,23 +456,24 @@ __device__ __forceinline__ void leaf_test(const float* r, f3 o, f3 d, float a2, 
     const float t = -((a.x * o.x + a.y * o.y + a.z * o.z) + a.w) / nd;
     if (!key_accept(t, key, best_t, best_key)) return;
     const f3 P = add(o, scale(t, d));
-    const float4 e0 = *reinterpret_cast<const float4*>(q + 4);
-    const float4 e1 = *reinterpret_cast<const float4*>(q + 8);
-    const float4 e2 = *reinterpret_cast<const float4*>(q + 12);
-    const float4 e3 = *reinterpret_cast<const float4*>(q + 16);
-    const float4 e4 = *reinterpret_cast<const float4*>(q + 20);
-    bool inside = !(dot(mk(e0.w, e1.x, e1.y), sub(P, mk(e0.x, e0.y, e0.z))) < 0.0f) &&
-                  !(dot(mk(e2.y, e2.z, e2.w), sub(P, mk(e1.z, e1.w, e2.x))) < 0.0f) &&
-                  !(dot(mk(e3.w, e4.x, e4.y), sub(P, mk(e3.x, e3.y, e3.z))) < 0.0f);
-    if (kind == 3 && inside) {
-        const float4 e5 = *reinterpret_cast<const float4*>(q + 24);
-        inside = !(dot(mk(e5.y, e5.z, e5.w), sub(P, mk(e4.z, e4.w, e5.x))) < 0.0f);
+    // the edge tests in order, each loading only its own {v_k, in_k}: a lane
+    // whose point fails an edge requests no further record bytes (the walk
+    // is bound by its L1 / L2 request traffic); same tests, same result
+    const float4 e0 = *reinterpret_cast<const float4*>(q + 4);   // v0.xyz in0.x
+    const float4 e1 = *reinterpret_cast<const float4*>(q + 8);   // in0.yz v1.xy
+    if (dot(mk(e0.w, e1.x, e1.y), sub(P, mk(e0.x, e0.y, e0.z))) < 0.0f) return;
+    const float4 e2 = *reinterpret_cast<const float4*>(q + 12);  // v1.z in1.xyz
+    if (dot(mk(e2.y, e2.z, e2.w), sub(P, mk(e1.z, e1.w, e2.x))) < 0.0f) return;
+    const float4 e3 = *reinterpret_cast<const float4*>(q + 16);  // v2.xyz in2.x
+    const float4 e4 = *reinterpret_cast<const float4*>(q + 20);  // in2.yz (v3.xy)
+    if (dot(mk(e3.w, e4.x, e4.y), sub(P, mk(e3.x, e3.y, e3.z))) < 0.0f) return;
+    if (kind == 3) {
+        const float4 e5 = *reinterpret_cast<const float4*>(q + 24);  // v3.z in3.xyz
+        if (dot(mk(e5.y, e5.z, e5.w), sub(P, mk(e4.z, e4.w, e5.x))) < 0.0f) return;
     }
-    if (inside) {
-        best_t = t;
-        best_id = id;
-        best_key = key;
-    }
+    best_t = t;
+    best_id = id;
+    best_key = key;
 }
 
 __device__ __forceinline__ void prim_test(const rt_kparams& K, int id, f3 o, f3 d, float a2, float a4, float& best_t,
