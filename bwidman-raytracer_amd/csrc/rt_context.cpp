@@ -11,6 +11,7 @@
 // the reference's order, so the kernel sees bit-identical inputs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -502,6 +503,272 @@ struct BvhBuilder {
         }
     }
 
+    // ---- spatial splits (SBVH, Stich, Friedrich & Dietrich 2009) ----------
+    // A reference is a primitive cut down to a region of space: its box
+    // bounds the part of the primitive inside every split plane it was cut
+    // by (polygons clipped in double precision, spheres by their box).  A
+    // primitive may sit in several leaves; testing it more than once changes
+    // nothing ((t, key) acceptance), and the union of its references' boxes
+    // covers the whole primitive.  Boxes are inflated as above when stored.
+    struct Ref {
+        double lo[3], hi[3];
+        int id;
+    };
+    std::vector<double> geo;  // per primitive id: up to 4 vertices, 12 doubles
+    std::vector<int> geo_nv;  // 3 / 4: polygon vertices; 0: clipped by its box
+    double root_area = 0.0;
+    size_t ref_budget = 0, n_refs = 0;
+    double split_alpha = 1e-5;  // try spatial splits when the object split's children overlap > alpha * root area
+    static constexpr int kSpatialBins = 32;
+
+    static double dinflate(double v) { return 1e-3 + 1e-4 * std::fabs(v); }
+    static float fdown(double v) {
+        float f = (float)v;
+        if ((double)f > v) f = std::nextafter(f, -INFINITY);
+        return f;
+    }
+    static float fup(double v) {
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, INFINITY);
+        return f;
+    }
+    static double darea(const double* lo, const double* hi) {
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return (dx < 0 || dy < 0 || dz < 0) ? 0.0 : 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+
+    // the part of r with s0 <= x_a <= s1; false if there is none
+    bool clip(const Ref& r, int a, double s0, double s1, Ref& out) const {
+        out = r;
+        out.lo[a] = std::max(r.lo[a], s0);
+        out.hi[a] = std::min(r.hi[a], s1);
+        if (out.lo[a] > out.hi[a]) return false;
+        const int nv = geo_nv[r.id];
+        if (nv < 3) return true;
+        double poly[8][3], tmp[8][3];
+        int n = nv;
+        for (int k = 0; k < nv; k++)
+            for (int q = 0; q < 3; q++) poly[k][q] = geo[(size_t)12 * r.id + 3 * k + q];
+        for (int side = 0; side < 2 && n > 0; side++) {
+            int m = 0;
+            for (int k = 0; k < n; k++) {
+                const double* p = poly[k];
+                const double* q = poly[(k + 1) % n];
+                const double dp = side == 0 ? p[a] - s0 : s1 - p[a];
+                const double dq = side == 0 ? q[a] - s0 : s1 - q[a];
+                if (dp >= 0.0)
+                    for (int c = 0; c < 3; c++) tmp[m][c] = p[c];
+                if (dp >= 0.0) m++;
+                if ((dp >= 0.0) != (dq >= 0.0)) {
+                    const double t = dp / (dp - dq);
+                    for (int c = 0; c < 3; c++) tmp[m][c] = p[c] + t * (q[c] - p[c]);
+                    m++;
+                }
+            }
+            n = m;
+            for (int k = 0; k < n; k++)
+                for (int c = 0; c < 3; c++) poly[k][c] = tmp[k][c];
+        }
+        // no part of the polygon in the slab (a sliver on its boundary is
+        // covered by the neighbouring reference's inflated box)
+        if (n == 0) return false;
+        double plo[3] = {INFINITY, INFINITY, INFINITY}, phi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int k = 0; k < n; k++)
+            for (int c = 0; c < 3; c++) {
+                plo[c] = std::min(plo[c], poly[k][c]);
+                phi[c] = std::max(phi[c], poly[k][c]);
+            }
+        for (int c = 0; c < 3; c++) {
+            out.lo[c] = std::max(out.lo[c], plo[c]);
+            out.hi[c] = std::min(out.hi[c], phi[c]);
+            if (out.lo[c] > out.hi[c]) {  // rounding: keep a degenerate box at the slab
+                out.lo[c] = out.hi[c] = std::min(std::max(0.5 * (plo[c] + phi[c]), out.lo[c]), out.hi[c]);
+            }
+        }
+        return true;
+    }
+
+    int build_s(std::vector<Ref>& refs) {
+        const int node = (int)tree.size();
+        tree.emplace_back();
+        const int n = (int)refs.size();
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (const Ref& r : refs)
+            for (int a = 0; a < 3; a++) {
+                lo[a] = std::min(lo[a], r.lo[a]);
+                hi[a] = std::max(hi[a], r.hi[a]);
+                const double c = 0.5 * (r.lo[a] + r.hi[a]);
+                clo[a] = std::min(clo[a], c);
+                chi[a] = std::max(chi[a], c);
+            }
+        for (int a = 0; a < 3; a++) {
+            tree[node].lo[a] = fdown(lo[a] - dinflate(lo[a]));
+            tree[node].hi[a] = fup(hi[a] + dinflate(hi[a]));
+        }
+        auto leaf = [&]() {
+            tree[node].first = (int)prims.size();
+            tree[node].count = n;
+            for (const Ref& r : refs) prims.push_back(r.id);
+            return node;
+        };
+        if (n <= 2) return leaf();
+        // object split: binned SAH over the reference centroids
+        double best_cost = INFINITY, ov_area = 0.0;
+        int best_axis = -1, best_bin = -1;
+        for (int a = 0; a < 3; a++) {
+            const double ext = chi[a] - clo[a];
+            if (!(ext > 0.0)) continue;
+            int cnt[kBins] = {0};
+            double blo[kBins][3], bhi[kBins][3];
+            for (int k = 0; k < kBins; k++)
+                for (int q = 0; q < 3; q++) blo[k][q] = INFINITY, bhi[k][q] = -INFINITY;
+            for (const Ref& r : refs) {
+                int k = (int)((0.5 * (r.lo[a] + r.hi[a]) - clo[a]) / ext * kBins);
+                k = std::min(std::max(k, 0), kBins - 1);
+                cnt[k]++;
+                for (int q = 0; q < 3; q++) blo[k][q] = std::min(blo[k][q], r.lo[q]), bhi[k][q] = std::max(bhi[k][q], r.hi[q]);
+            }
+            double rl[kBins][3], rh[kBins][3];
+            int rc[kBins];
+            double al[3] = {INFINITY, INFINITY, INFINITY}, ah[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int c = 0;
+            for (int k = kBins - 1; k > 0; k--) {
+                c += cnt[k];
+                for (int q = 0; q < 3; q++) al[q] = std::min(al[q], blo[k][q]), ah[q] = std::max(ah[q], bhi[k][q]);
+                for (int q = 0; q < 3; q++) rl[k][q] = al[q], rh[k][q] = ah[q];
+                rc[k] = c;
+            }
+            double ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int lc = 0;
+            for (int k = 0; k < kBins - 1; k++) {
+                lc += cnt[k];
+                for (int q = 0; q < 3; q++) ll[q] = std::min(ll[q], blo[k][q]), lh[q] = std::max(lh[q], bhi[k][q]);
+                if (lc == 0 || rc[k + 1] == 0) continue;
+                const double cost = darea(ll, lh) * lc + darea(rl[k + 1], rh[k + 1]) * rc[k + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = a;
+                    best_bin = k;
+                    double ol[3], oh[3];
+                    for (int q = 0; q < 3; q++) ol[q] = std::max(ll[q], rl[k + 1][q]), oh[q] = std::min(lh[q], rh[k + 1][q]);
+                    ov_area = darea(ol, oh);
+                }
+            }
+        }
+        // spatial split: chop the references into spatial bins
+        bool spatial = false;
+        double split_pos = 0.0;
+        if (n_refs < ref_budget && ov_area > split_alpha * root_area) {
+            for (int a = 0; a < 3; a++) {
+                const double ext = hi[a] - lo[a];
+                if (!(ext > 0.0)) continue;
+                const double w = ext / kSpatialBins;
+                int ent[kSpatialBins] = {0}, ext_[kSpatialBins] = {0};
+                double blo[kSpatialBins][3], bhi[kSpatialBins][3];
+                for (int k = 0; k < kSpatialBins; k++)
+                    for (int q = 0; q < 3; q++) blo[k][q] = INFINITY, bhi[k][q] = -INFINITY;
+                for (const Ref& r : refs) {
+                    int k0 = (int)((r.lo[a] - lo[a]) / w), k1 = (int)((r.hi[a] - lo[a]) / w);
+                    k0 = std::min(std::max(k0, 0), kSpatialBins - 1);
+                    k1 = std::min(std::max(k1, k0), kSpatialBins - 1);
+                    bool any = false;
+                    int first = -1, last = -1;
+                    for (int k = k0; k <= k1; k++) {
+                        const double s0 = k == 0 ? -INFINITY : lo[a] + k * w;
+                        const double s1 = k == kSpatialBins - 1 ? INFINITY : lo[a] + (k + 1) * w;
+                        Ref part;
+                        if (!clip(r, a, s0, s1, part)) continue;
+                        any = true;
+                        if (first < 0) first = k;
+                        last = k;
+                        for (int q = 0; q < 3; q++) blo[k][q] = std::min(blo[k][q], part.lo[q]), bhi[k][q] = std::max(bhi[k][q], part.hi[q]);
+                    }
+                    if (!any) {  // (rounding) count it in its box's first bin
+                        first = last = k0;
+                        for (int q = 0; q < 3; q++) blo[k0][q] = std::min(blo[k0][q], r.lo[q]), bhi[k0][q] = std::max(bhi[k0][q], r.hi[q]);
+                    }
+                    ent[first]++;
+                    ext_[last]++;
+                }
+                double rl[kSpatialBins][3], rh[kSpatialBins][3];
+                int rc[kSpatialBins];
+                double al[3] = {INFINITY, INFINITY, INFINITY}, ah[3] = {-INFINITY, -INFINITY, -INFINITY};
+                int c = 0;
+                for (int k = kSpatialBins - 1; k > 0; k--) {
+                    c += ext_[k];
+                    for (int q = 0; q < 3; q++) al[q] = std::min(al[q], blo[k][q]), ah[q] = std::max(ah[q], bhi[k][q]);
+                    for (int q = 0; q < 3; q++) rl[k][q] = al[q], rh[k][q] = ah[q];
+                    rc[k] = c;
+                }
+                double ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+                int lc = 0;
+                for (int k = 0; k < kSpatialBins - 1; k++) {
+                    lc += ent[k];
+                    for (int q = 0; q < 3; q++) ll[q] = std::min(ll[q], blo[k][q]), lh[q] = std::max(lh[q], bhi[k][q]);
+                    if (lc == 0 || rc[k + 1] == 0) continue;
+                    const double cost = darea(ll, lh) * lc + darea(rl[k + 1], rh[k + 1]) * rc[k + 1];
+                    if (cost < best_cost) {
+                        best_cost = cost;
+                        best_axis = a;
+                        spatial = true;
+                        split_pos = lo[a] + (k + 1) * w;
+                    }
+                }
+            }
+        }
+        const double leaf_cost = darea(lo, hi) * n;
+        best_cost += trav_cost * darea(lo, hi);
+        if (best_axis < 0 || (best_cost >= leaf_cost && n <= max_leaf)) {
+            if (n <= max_leaf) return leaf();
+        }
+        std::vector<Ref> L, R;
+        if (best_axis >= 0 && spatial) {
+            const int a = best_axis;
+            for (const Ref& r : refs) {
+                if (r.hi[a] <= split_pos) {
+                    L.push_back(r);
+                } else if (r.lo[a] >= split_pos) {
+                    R.push_back(r);
+                } else {
+                    Ref pl, pr;
+                    const bool hl = clip(r, a, -INFINITY, split_pos, pl), hr = clip(r, a, split_pos, INFINITY, pr);
+                    if (hl) L.push_back(pl);
+                    if (hr) R.push_back(pr);
+                    if (!hl && !hr) L.push_back(r);
+                }
+            }
+        } else if (best_axis >= 0) {
+            const int a = best_axis;
+            const double ext = chi[a] - clo[a];
+            for (const Ref& r : refs) {
+                int k = (int)((0.5 * (r.lo[a] + r.hi[a]) - clo[a]) / ext * kBins);
+                k = std::min(std::max(k, 0), kBins - 1);
+                (k <= best_bin ? L : R).push_back(r);
+            }
+        }
+        if (L.empty() || R.empty()) {  // no usable split: halve the list along the widest centroid axis
+            L.clear();
+            R.clear();
+            int a = 0;
+            for (int q = 1; q < 3; q++)
+                if (chi[q] - clo[q] > chi[a] - clo[a]) a = q;
+            std::sort(refs.begin(), refs.end(),
+                      [a](const Ref& x, const Ref& y) { return x.lo[a] + x.hi[a] < y.lo[a] + y.hi[a]; });
+            L.assign(refs.begin(), refs.begin() + n / 2);
+            R.assign(refs.begin() + n / 2, refs.end());
+            best_axis = a;
+        }
+        n_refs += L.size() + R.size() - (size_t)n;
+        std::vector<Ref>().swap(refs);
+        const int l = build_s(L);
+        const int r = build_s(R);
+        tree[node].axis = best_axis;
+        tree[node].left = l;
+        tree[node].right = r;
+        return node;
+    }
+
     void add(int id, const float* lo, const float* hi) {
         BvhItem it;
         for (int a = 0; a < 3; a++) {
@@ -744,7 +1011,66 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             // bit clear (a negative value means "internal node" to the kernels)
             if (const char* e = std::getenv("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 127);
             if (const char* e = std::getenv("BWRT_BVH_CT")) B.trav_cost = (float)std::atof(e);
-            B.build(0, nb);
+            // spatial splits (BWRT_BVH_SBVH=0: object splits only), references
+            // up to BWRT_BVH_REFS x the primitives (default 2)
+            bool sbvh = true;
+            if (const char* e = std::getenv("BWRT_BVH_SBVH")) sbvh = std::atoi(e) != 0;
+            if (sbvh) {
+                B.geo.assign((size_t)12 * (ns + np + nt + nq), 0.0);
+                B.geo_nv.assign((size_t)(ns + np + nt + nq), 0);
+                auto geo = [&](int id, const rt_vec3* v, int nv) {
+                    B.geo_nv[id] = nv;
+                    for (int k = 0; k < nv; k++) {
+                        B.geo[(size_t)12 * id + 3 * k + 0] = v[k].x;
+                        B.geo[(size_t)12 * id + 3 * k + 1] = v[k].y;
+                        B.geo[(size_t)12 * id + 3 * k + 2] = v[k].z;
+                    }
+                };
+                for (int i = 0; i < nt; i++) geo(ns + np + i, s->triangles[i].vertices, 3);
+                for (int i = 0; i < nq; i++) geo(ns + np + nt + i, s->quads[i].vertices, 4);
+                std::vector<BvhBuilder::Ref> refs;
+                refs.reserve(nb);
+                double rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                auto addref = [&](int id, const double* lo, const double* hi) {
+                    BvhBuilder::Ref r;
+                    for (int a = 0; a < 3; a++) {
+                        r.lo[a] = lo[a];
+                        r.hi[a] = hi[a];
+                        rlo[a] = std::min(rlo[a], lo[a]);
+                        rhi[a] = std::max(rhi[a], hi[a]);
+                    }
+                    r.id = id;
+                    refs.push_back(r);
+                };
+                for (int i = 0; i < ns; i++) {
+                    const rt_sphere& sp = s->spheres[i];
+                    const double r = std::fabs((double)sp.radius);
+                    const double lo[3] = {sp.position.x - r, sp.position.y - r, sp.position.z - r};
+                    const double hi[3] = {sp.position.x + r, sp.position.y + r, sp.position.z + r};
+                    addref(i, lo, hi);
+                }
+                auto polyref = [&](int id, const rt_vec3* v, int nv) {
+                    double lo[3] = {v[0].x, v[0].y, v[0].z}, hi[3] = {v[0].x, v[0].y, v[0].z};
+                    for (int k = 1; k < nv; k++) {
+                        const double p[3] = {v[k].x, v[k].y, v[k].z};
+                        for (int a = 0; a < 3; a++) lo[a] = std::min(lo[a], p[a]), hi[a] = std::max(hi[a], p[a]);
+                    }
+                    addref(id, lo, hi);
+                };
+                for (int i = 0; i < nt; i++) polyref(ns + np + i, s->triangles[i].vertices, 3);
+                for (int i = 0; i < nq; i++) polyref(ns + np + nt + i, s->quads[i].vertices, 4);
+                double refs_x = 2.0;
+                if (const char* e = std::getenv("BWRT_BVH_REFS")) refs_x = std::atof(e);
+                if (const char* e = std::getenv("BWRT_BVH_ALPHA")) B.split_alpha = std::atof(e);
+                B.root_area = BvhBuilder::darea(rlo, rhi);
+                B.ref_budget = (size_t)(refs_x * nb);
+                B.n_refs = (size_t)nb;
+                B.build_s(refs);
+                if (B.prims.size() >= (1u << 24))
+                    return fail(c, RT_ERR_UNSUPPORTED, "%zu BVH references: at most 2^24 - 1", B.prims.size());
+            } else {
+                B.build(0, nb);
+            }
             // octant arrays only along the scene's long axes (extent >= half
             // the longest): each bit doubles the node data the walks spread
             // over the caches, and a short axis buys little front-to-back
@@ -764,8 +1090,8 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
                 long ax[3] = {0, 0, 0}, inner = 0;
                 for (const BvhNode& t : B.tree)
                     if (t.left >= 0) ax[t.axis]++, inner++;
-                std::fprintf(stderr, "bvh: %d nodes, %ld internal, split axes x %ld y %ld z %ld, octant mask %d, n16 %d\n",
-                             (int)B.tree.size(), inner, ax[0], ax[1], ax[2], B.order_mask, B.n16 ? 1 : 0);
+                std::fprintf(stderr, "bvh: %d nodes, %ld internal, %zu references of %d primitives, split axes x %ld y %ld z %ld, octant mask %d, n16 %d\n",
+                             (int)B.tree.size(), inner, B.prims.size(), nb, ax[0], ax[1], ax[2], B.order_mask, B.n16 ? 1 : 0);
             }
             c->bvh_nodes_per_order = B.n_nodes;
             c->bvh_order_mask = B.order_mask;
