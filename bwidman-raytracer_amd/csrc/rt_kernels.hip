@@ -1454,8 +1454,11 @@ rt_render_sorted_kernel(rt_kparams K) {
 // (t, RT_KEY) acceptance are exactly those of closest_hit_bvh (planes
 // first, then every primitive of every leaf whose inflated box the ray may
 // enter), so the result does not depend on when the lane walks.
+// refill threshold: with the spatial-split tree, config 5 at 40 / 44 / 48 /
+// 52 / 56: 124.9 / 122.9 / 122.3 / 122.6 / 123.9 ms, its 1/8 shard 26.9 /
+// 26.9 / 27.0 / 27.1 / 28.8 ms
 #ifndef RT_REFILL
-#define RT_REFILL 40
+#define RT_REFILL 48
 #endif
 // fp16 bits -> float (exact)
 __device__ __forceinline__ float h2f(unsigned bits) {
