@@ -1096,7 +1096,9 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             c->bvh_nodes_per_order = B.n_nodes;
             c->bvh_order_mask = B.order_mask;
             off_bvh = (total + 3) & ~(size_t)3;
-            off_bvh_prims = off_bvh + B.nodes.size();  // leaf records, RT_LEAF_FLOATS each
+            // leaf records, RT_LEAF_FLOATS (128 B) each, and the 16-byte nodes
+            // start on 128-byte boundaries: a record spans one cache line
+            off_bvh_prims = (off_bvh + B.nodes.size() + 31) & ~(size_t)31;
             off_bvh16 = B.n16 ? off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS : 0;
             h.resize(off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS + (B.n16 ? B.nodes16.size() : 0) + 4, 0.0f);
             std::memcpy(h.data() + off_bvh, B.nodes.data(), B.nodes.size() * sizeof(float));
@@ -1108,10 +1110,10 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
                 const float* src;
                 if (id < ns) {
                     kind = 0, idx = id, nf = RT_SPH_FLOATS, src = h.data() + (size_t)idx * RT_SPH_FLOATS;
-                } else if (id < ns + np + nt) {
-                    kind = 2, idx = id - ns - np, nf = RT_TRI_FLOATS, src = h.data() + off_tri + (size_t)idx * RT_TRI_FLOATS;
+                } else if (id < ns + np + nt) {  // (the BVH does not cull: no cull sphere)
+                    kind = 2, idx = id - ns - np, nf = RT_TRI_CULL, src = h.data() + off_tri + (size_t)idx * RT_TRI_FLOATS;
                 } else {
-                    kind = 3, idx = id - ns - np - nt, nf = RT_QUAD_FLOATS,
+                    kind = 3, idx = id - ns - np - nt, nf = RT_QUAD_CULL,
                     src = h.data() + off_quad + (size_t)idx * RT_QUAD_FLOATS;
                 }
                 const int key = RT_KEY(kind, idx), zero = 0;

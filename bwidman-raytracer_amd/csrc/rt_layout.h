@@ -35,7 +35,7 @@
 #define RT_QUAD_FLOATS 32
 #define RT_TRI_CULL 24   // offset of the cull sphere in a triangle record
 #define RT_QUAD_CULL 28
-#define RT_LEAF_FLOATS 36  // BVH leaf record: 4 header + up to 32 record floats
+#define RT_LEAF_FLOATS 32  // BVH leaf record: 4 header + the record without its cull sphere (<= 28 floats)
 #define RT_HIT_FLOATS 16
 
 #define RT_NEAR_ZERO 0.0001f       // Intersection.cuh:4
