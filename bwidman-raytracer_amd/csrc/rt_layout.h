@@ -36,7 +36,9 @@
 #define RT_TRI_CULL 24   // offset of the cull sphere in a triangle record
 #define RT_QUAD_CULL 28
 #define RT_LEAF_FLOATS 32  // BVH leaf record: 4 header + the record without its cull sphere (<= 28 floats)
+#ifndef RT_HIT_FLOATS
 #define RT_HIT_FLOATS 16
+#endif
 
 #define RT_NEAR_ZERO 0.0001f       // Intersection.cuh:4
 #define RT_SPECULAR_CHANCE 0.5f    // Main.cu:29
