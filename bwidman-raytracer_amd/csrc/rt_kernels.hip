@@ -1460,6 +1460,13 @@ rt_render_sorted_kernel(rt_kparams K) {
 #ifndef RT_REFILL
 #define RT_REFILL 48
 #endif
+// leaf-test batch threshold (lanes of 64 ready): config 5 at 52 / 54 / 56 / 58
+// / 60 / 62 / 64 (all lanes, Aila & Laine's rule): 102.2 / 99.1 / 98.1 / 97.3
+// / 98.2 / 101.1 / 118.0 ms, its 1/8 shard 24.8 / 23.4 / 23.0 / 22.3 / 22.2 /
+// 22.3 / 25.5 ms
+#ifndef RT_LEAF_THRESH
+#define RT_LEAF_THRESH 58
+#endif
 // fp16 bits -> float (exact)
 __device__ __forceinline__ float h2f(unsigned bits) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)(bits & 0xffffu));
@@ -1657,7 +1664,10 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                     leaf = park ? lf : leaf;
                     node = !hit || park ? miss : (is_leaf ? node : node + 1);
                 }
-                if (__all(!walking || leaf >= 0 || node < 0 || stalled)) break;
+                // test the parked leaves once RT_LEAF_THRESH of the 64 lanes are
+                // ready (a leaf parked, the walk done or stalled, no walk);
+                // the rest walk on and join a later batch
+                if (__popcll(__ballot(!walking || leaf >= 0 || node < 0 || stalled)) >= RT_LEAF_THRESH) break;
             }
             if (leaf >= 0) {
                 const int first = leaf & 0xffffff, count = leaf >> 24;
