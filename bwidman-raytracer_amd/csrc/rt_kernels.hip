@@ -1454,11 +1454,12 @@ rt_render_sorted_kernel(rt_kparams K) {
 // (t, RT_KEY) acceptance are exactly those of closest_hit_bvh (planes
 // first, then every primitive of every leaf whose inflated box the ray may
 // enter), so the result does not depend on when the lane walks.
-// refill threshold: with the spatial-split tree, config 5 at 40 / 44 / 48 /
-// 52 / 56: 124.9 / 122.9 / 122.3 / 122.6 / 123.9 ms, its 1/8 shard 26.9 /
-// 26.9 / 27.0 / 27.1 / 28.8 ms
+// refill threshold (of 64, relative to the lanes that still hold a pixel):
+// with the spatial-split tree and leaf batches at 58 ready lanes, config 5 at
+// 32 / 36 / 40 / 48: 96.4 / 95.0 / 94.9 / 97.8 ms, its 1/8 shard 21.6 / 21.6
+// / 22.1 / 22.3 ms
 #ifndef RT_REFILL
-#define RT_REFILL 48
+#define RT_REFILL 36
 #endif
 // leaf-test batch threshold (lanes of 64 ready): config 5 at 52 / 54 / 56 / 58
 // / 60 / 62 / 64 (all lanes, Aila & Laine's rule): 102.2 / 99.1 / 98.1 / 97.3
