@@ -1466,7 +1466,7 @@ rt_render_sorted_kernel(rt_kparams K) {
 // / 98.2 / 101.1 / 118.0 ms, its 1/8 shard 24.8 / 23.4 / 23.0 / 22.3 / 22.2 /
 // 22.3 / 25.5 ms
 #ifndef RT_LEAF_THRESH
-#define RT_LEAF_THRESH 58
+#define RT_LEAF_THRESH 60
 #endif
 // fp16 bits -> float (exact)
 __device__ __forceinline__ float h2f(unsigned bits) {
@@ -1497,7 +1497,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     bool walking = false;    // a BVH walk is in flight
     bool pending = false;    // a finished query waits to be shaded
     bool idle = false;       // no pixel left
-    int node = -1, leaf = -1;
+    int node = -1, leaf = -1, leaf2 = -1;  // two parked leaves per lane
     float best_t = INFINITY;
     int best_id = -1, best_key = -1;
     f3 inv = o, oinv = o;
@@ -1627,13 +1627,14 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 nodes = K.bvh_nodes + (size_t)order * K.bvh_order_stride;
             node = 0;
             leaf = -1;
+            leaf2 = -1;
             walking = true;
         }
         if (__ballot(walking) == 0ull) break;  // every lane idle
 
         // (B) walk until RT_REFILL lanes are waiting for a new ray
         while (true) {
-            while (true) {  // node steps; a lane parks the first leaf its ray enters
+            while (true) {  // node steps; a lane parks the first two leaves its ray enters
                 bool stalled = false;
                 if (walking && node >= 0) {
                     RT_BRANCH_COUNT(K, 5);
@@ -1658,11 +1659,12 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                     const int miss = __float_as_int(lo.w);
                     const int lf = __float_as_int(hi.w);
                     // branch-free step: miss -> skip the subtree; internal -> first
-                    // child; leaf -> park it (or stall on a second one)
+                    // child; leaf -> park it (or stall on a third one)
                     const bool is_leaf = hit && lf >= 0;
-                    stalled = is_leaf && leaf >= 0;
-                    const bool park = is_leaf && leaf < 0;
-                    leaf = park ? lf : leaf;
+                    stalled = is_leaf && leaf2 >= 0;
+                    const bool park = is_leaf && leaf2 < 0;
+                    leaf2 = park && leaf >= 0 ? lf : leaf2;
+                    leaf = park && leaf < 0 ? lf : leaf;
                     node = !hit || park ? miss : (is_leaf ? node : node + 1);
                 }
                 // test the parked leaves once RT_LEAF_THRESH of the 64 lanes are
@@ -1678,6 +1680,13 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                               best_key);
                 }
                 leaf = -1;
+            }
+            if (leaf2 >= 0) {
+                const int first = leaf2 & 0xffffff, count = leaf2 >> 24;
+                for (int k = 0; k < count; k++)
+                    leaf_test(K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
+                              best_key);
+                leaf2 = -1;
             }
             if (walking && node < 0) {  // walk complete: the query result is best_t / best_id
                 walking = false;
