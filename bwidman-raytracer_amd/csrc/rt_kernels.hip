@@ -1505,8 +1505,29 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     const float* nodes = K.bvh_nodes;
     const unsigned* nodes16 = K.bvh_nodes16;
     const int nn = K.bvh_n_nodes;
+#ifdef RT_STAMPS
+    // diagnostic: wave cycles in (A) refill, node steps, leaf tests ->
+    // K.stamps[0..2]; [3] refill passes, [4] node-loop iterations, [5] leaf batches
+    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(k)                                              \
+    do {                                                      \
+        unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+        st_acc[k] += _t - st_prev;                            \
+        st_prev = _t;                                         \
+    } while (0)
+#define COUNT(k) (st_acc[k] += 1)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#define COUNT(k) \
+    do {         \
+    } while (0)
+#endif
 
     while (true) {
+        COUNT(3);
         // (A) lanes without a walk: shade the finished query, start the next ray
         while (!walking && !idle) {
             if (pending) {
@@ -1630,6 +1651,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             leaf2 = -1;
             walking = true;
         }
+        STAMP(0);
         if (__ballot(walking) == 0ull) break;  // every lane idle
 
         // (B) walk until RT_REFILL lanes are waiting for a new ray
@@ -1670,8 +1692,11 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 // test the parked leaves once RT_LEAF_THRESH of the 64 lanes are
                 // ready (a leaf parked, the walk done or stalled, no walk);
                 // the rest walk on and join a later batch
+                COUNT(4);
                 if (__popcll(__ballot(!walking || leaf >= 0 || node < 0 || stalled)) >= RT_LEAF_THRESH) break;
             }
+            STAMP(1);
+            COUNT(5);
             if (leaf >= 0) {
                 const int first = leaf & 0xffffff, count = leaf >> 24;
                 for (int k = 0; k < count; k++) {
@@ -1688,6 +1713,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                               best_key);
                 leaf2 = -1;
             }
+            STAMP(2);
             if (walking && node < 0) {  // walk complete: the query result is best_t / best_id
                 walking = false;
                 pending = true;
@@ -1699,6 +1725,12 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             if (w == 0ull || 64 * __popcll(__ballot(!walking && !idle)) >= RT_REFILL * __popcll(__ballot(!idle))) break;
         }
     }
+#ifdef RT_STAMPS
+    if ((threadIdx.x & 63) == 0 && K.stamps)
+        for (int k = 0; k < 6; k++) atomicAdd(&K.stamps[k], st_acc[k]);
+#endif
+#undef STAMP
+#undef COUNT
 }
 #endif  // RT_TU_BVH
 
