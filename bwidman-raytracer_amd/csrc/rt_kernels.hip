@@ -451,16 +451,18 @@ __device__ __forceinline__ void leaf_test(const float* r, f3 o, f3 d, float a2, 
         return;
     }
     const float* q = r + 4;  // triangle / quad record {n, d, (v_k, in_k)...}
+    // the first edge's record is loaded with the plane (one memory round
+    // trip less: config 5 91.8 -> 91.0 ms)
+    const float4 e0 = *reinterpret_cast<const float4*>(q + 4);   // v0.xyz in0.x
+    const float4 e1 = *reinterpret_cast<const float4*>(q + 8);   // in0.yz v1.xy
     const float nd = a.x * d.x + a.y * d.y + a.z * d.z;
     if (fabsf(nd) < RT_NEAR_ZERO) return;
     const float t = -((a.x * o.x + a.y * o.y + a.z * o.z) + a.w) / nd;
     if (!key_accept(t, key, best_t, best_key)) return;
     const f3 P = add(o, scale(t, d));
-    // the edge tests in order, each loading only its own {v_k, in_k}: a lane
-    // whose point fails an edge requests no further record bytes (the walk
-    // is bound by its L1 / L2 request traffic); same tests, same result
-    const float4 e0 = *reinterpret_cast<const float4*>(q + 4);   // v0.xyz in0.x
-    const float4 e1 = *reinterpret_cast<const float4*>(q + 8);   // in0.yz v1.xy
+    // the later edge tests in order, each loading only its own {v_k, in_k}:
+    // a lane whose point fails an edge requests no further record bytes (the
+    // walk is bound by its L1 / L2 request traffic); same tests, same result
     if (dot(mk(e0.w, e1.x, e1.y), sub(P, mk(e0.x, e0.y, e0.z))) < 0.0f) return;
     const float4 e2 = *reinterpret_cast<const float4*>(q + 12);  // v1.z in1.xyz
     if (dot(mk(e2.y, e2.z, e2.w), sub(P, mk(e1.z, e1.w, e2.x))) < 0.0f) return;
