@@ -189,15 +189,16 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
+    t_issued = time.perf_counter()  # host time to enqueue the steps (must stay below the GPU time)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in events]
-    t = torch.tensor([elapsed, sum(kern_ms) / len(kern_ms)], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, sum(kern_ms) / len(kern_ms), t_issued - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_avg_ms = float(t[0]), float(t[1])
+    elapsed, kern_avg_ms, issue_s = float(t[0]), float(t[1]), float(t[2])
 
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
@@ -229,6 +230,8 @@ def main():
                        + (" (frames pipelined: gather of frame k overlaps render of k+1)" if overlap else "")},
             "ms_per_frame": round(ms_step, 4),
             "kernel_ms_avg": round(kern_avg_ms, 4),
+            # host time to enqueue one step (render + gather calls), max over ranks
+            "host_issue_ms_per_step": round(issue_s / args.steps * 1e3, 4),
             "queries_per_frame": QUERIES_PER_FRAME.get(args.config),
             "actual_Msegments_per_s": (round(QUERIES_PER_FRAME[args.config] * args.steps / elapsed / 1e6, 1)
                                        if args.config in QUERIES_PER_FRAME else None),
