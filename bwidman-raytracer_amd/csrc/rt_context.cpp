@@ -113,6 +113,7 @@ struct rt_context {
     size_t host_rgba_bytes = 0;
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
     int tile_w = -1;             // BWRT_TILE: wave tile width (0 = linear order; -1 = launch policy)
+    int leaf_batch = -1;         // BWRT_LEAF_BATCH: BVH refill kernel leaf-batch threshold (-1 = launch policy)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
 };
@@ -828,6 +829,7 @@ int rt_create(int device, rt_context** out) {
         if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
     }
     if (const char* g = std::getenv("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
+    if (const char* g = std::getenv("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = std::getenv("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
     if (const char* g = std::getenv("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
     *out = c;
@@ -1377,6 +1379,10 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     // together in the tree (config 5: 170.4 -> 167.7 ms; at 1/8 38.5 -> 35.2)
     const bool small = (long)K.rows * K.width <= (long)c->num_cus * 1024;
     K.tile_w = c->tile_w >= 0 ? c->tile_w : K.bvh_nodes ? (small ? 4 : 8) : (small ? 32 : 16);
+    // BVH refill kernel: test the parked leaves once this many of a wave's 64
+    // lanes are ready; small shards (every wave resident at once, the frame
+    // ends with the slowest waves) batch later
+    K.leaf_batch = c->leaf_batch > 0 ? c->leaf_batch : small ? RT_LEAF_BATCH_SMALL : RT_LEAF_BATCH;
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
     if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {

@@ -1463,13 +1463,11 @@ rt_render_sorted_kernel(rt_kparams K) {
 #ifndef RT_REFILL
 #define RT_REFILL 36
 #endif
-// leaf-test batch threshold (lanes of 64 ready): config 5 at 52 / 54 / 56 / 58
-// / 60 / 62 / 64 (all lanes, Aila & Laine's rule): 102.2 / 99.1 / 98.1 / 97.3
-// / 98.2 / 101.1 / 118.0 ms, its 1/8 shard 24.8 / 23.4 / 23.0 / 22.3 / 22.2 /
-// 22.3 / 25.5 ms
-#ifndef RT_LEAF_THRESH
-#define RT_LEAF_THRESH 60
-#endif
+// leaf-test batch threshold K.leaf_batch (lanes of 64 ready; rt_layout.h
+// RT_LEAF_BATCH): with one parked leaf, config 5 at 52 / 54 / 56 / 58 / 60 /
+// 62 / 64 (all lanes, Aila & Laine's rule): 102.2 / 99.1 / 98.1 / 97.3 / 98.2
+// / 101.1 / 118.0 ms, its 1/8 shard 24.8 / 23.4 / 23.0 / 22.3 / 22.2 / 22.3 /
+// 25.5 ms; with two, 60 / 62: 91.8 / 92.6 ms, 1/8 shard 21.3 / 20.2 ms
 // fp16 bits -> float (exact)
 __device__ __forceinline__ float h2f(unsigned bits) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)(bits & 0xffffu));
@@ -1691,11 +1689,11 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                     leaf = park && leaf < 0 ? lf : leaf;
                     node = !hit || park ? miss : (is_leaf ? node : node + 1);
                 }
-                // test the parked leaves once RT_LEAF_THRESH of the 64 lanes are
+                // test the parked leaves once K.leaf_batch of the 64 lanes are
                 // ready (a leaf parked, the walk done or stalled, no walk);
                 // the rest walk on and join a later batch
                 COUNT(4);
-                if (__popcll(__ballot(!walking || leaf >= 0 || node < 0 || stalled)) >= RT_LEAF_THRESH) break;
+                if (__popcll(__ballot(!walking || leaf >= 0 || node < 0 || stalled)) >= K.leaf_batch) break;
             }
             STAMP(1);
             COUNT(5);

@@ -112,7 +112,16 @@ struct rt_kparams {
     unsigned* group_cost;
     long order_n;               // grid the current group_order was built for (0 = none)
     long order_cap;             // capacity of group_order / group_cost
+    int leaf_batch;             // BVH refill kernel: leaf tests once this many lanes are ready
 };
+
+// leaf-batch thresholds of the launch policy (full frames / small shards)
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 60
+#endif
+#ifndef RT_LEAF_BATCH_SMALL
+#define RT_LEAF_BATCH_SMALL 62
+#endif
 
 // Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,
 // quad i, then i+1): a primitive's key; among equal distances the reference
