@@ -114,6 +114,7 @@ struct rt_context {
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
     int tile_w = -1;             // BWRT_TILE: wave tile width (0 = linear order; -1 = launch policy)
     int leaf_batch = -1;         // BWRT_LEAF_BATCH: BVH refill kernel leaf-batch threshold (-1 = launch policy)
+    int refill = -1;             // BWRT_REFILL: BVH refill kernel refill threshold (-1 = launch policy)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
 };
@@ -830,6 +831,7 @@ int rt_create(int device, rt_context** out) {
     }
     if (const char* g = std::getenv("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
     if (const char* g = std::getenv("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
+    if (const char* g = std::getenv("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = std::getenv("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
     if (const char* g = std::getenv("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
     *out = c;
@@ -1383,6 +1385,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     // lanes are ready; small shards (every wave resident at once, the frame
     // ends with the slowest waves) batch later
     K.leaf_batch = c->leaf_batch > 0 ? c->leaf_batch : small ? RT_LEAF_BATCH_SMALL : RT_LEAF_BATCH;
+    K.refill = c->refill > 0 ? c->refill : small ? RT_REFILL_SMALL : RT_REFILL;
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
     if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {

@@ -1448,7 +1448,7 @@ rt_render_sorted_kernel(rt_kparams K) {
 // ---- BVH kernel with ray refill (large scenes) --------------------------------
 // One path per lane like rt_render_kernel, but the BVH walk is not a
 // wave-synchronous call: each lane keeps its walk state (node, parked leaf,
-// closest hit) across iterations, and once RT_REFILL lanes of a wave have
+// closest hit) across iterations, and once K.refill lanes of a wave have
 // finished their walks, those lanes shade their hit and set up their next
 // ray while the others stay parked mid-walk (persistent traversal with ray
 // refill, Aila & Laine 2009), so the node loop runs on fuller waves instead
@@ -1456,13 +1456,10 @@ rt_render_sorted_kernel(rt_kparams K) {
 // (t, RT_KEY) acceptance are exactly those of closest_hit_bvh (planes
 // first, then every primitive of every leaf whose inflated box the ray may
 // enter), so the result does not depend on when the lane walks.
-// refill threshold (of 64, relative to the lanes that still hold a pixel):
-// with the spatial-split tree and leaf batches at 58 ready lanes, config 5 at
-// 32 / 36 / 40 / 48: 96.4 / 95.0 / 94.9 / 97.8 ms, its 1/8 shard 21.6 / 21.6
-// / 22.1 / 22.3 ms
-#ifndef RT_REFILL
-#define RT_REFILL 36
-#endif
+// refill threshold K.refill (of 64, relative to the lanes that still hold a
+// pixel; rt_layout.h RT_REFILL): with the spatial-split tree and leaf batches
+// at 58 ready lanes, config 5 at 32 / 36 / 40 / 48: 96.4 / 95.0 / 94.9 / 97.8
+// ms, its 1/8 shard 21.6 / 21.6 / 22.1 / 22.3 ms
 // leaf-test batch threshold K.leaf_batch (lanes of 64 ready; rt_layout.h
 // RT_LEAF_BATCH): with one parked leaf, config 5 at 52 / 54 / 56 / 58 / 60 /
 // 62 / 64 (all lanes, Aila & Laine's rule): 102.2 / 99.1 / 98.1 / 97.3 / 98.2
@@ -1654,7 +1651,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
         STAMP(0);
         if (__ballot(walking) == 0ull) break;  // every lane idle
 
-        // (B) walk until RT_REFILL lanes are waiting for a new ray
+        // (B) walk until K.refill lanes are waiting for a new ray
         while (true) {
             while (true) {  // node steps; a lane parks the first two leaves its ray enters
                 bool stalled = false;
@@ -1719,10 +1716,10 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 pending = true;
             }
             const unsigned long long w = __ballot(walking);
-            // RT_REFILL of 64 relative to the lanes that still have a pixel, so a
+            // K.refill of 64 relative to the lanes that still have a pixel, so a
             // wave's tail (pixels done, lanes idle) keeps refilling: config 5
             // 120.4 -> 117.4 ms, its 1/8 shard 26.6 -> 25.6 ms (absolute count)
-            if (w == 0ull || 64 * __popcll(__ballot(!walking && !idle)) >= RT_REFILL * __popcll(__ballot(!idle))) break;
+            if (w == 0ull || 64 * __popcll(__ballot(!walking && !idle)) >= K.refill * __popcll(__ballot(!idle))) break;
         }
     }
 #ifdef RT_STAMPS

@@ -113,6 +113,7 @@ struct rt_kparams {
     long order_n;               // grid the current group_order was built for (0 = none)
     long order_cap;             // capacity of group_order / group_cost
     int leaf_batch;             // BVH refill kernel: leaf tests once this many lanes are ready
+    int refill;                 // BVH refill kernel: new rays once this many of 64 (relative) wait
 };
 
 // leaf-batch thresholds of the launch policy (full frames / small shards)
@@ -121,6 +122,12 @@ struct rt_kparams {
 #endif
 #ifndef RT_LEAF_BATCH_SMALL
 #define RT_LEAF_BATCH_SMALL 62
+#endif
+#ifndef RT_REFILL
+#define RT_REFILL 36
+#endif
+#ifndef RT_REFILL_SMALL
+#define RT_REFILL_SMALL 36
 #endif
 
 // Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,
