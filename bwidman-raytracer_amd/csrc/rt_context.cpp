@@ -1120,12 +1120,11 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
                     kind = 3, idx = id - ns - np - nt, nf = RT_QUAD_CULL,
                     src = h.data() + off_quad + (size_t)idx * RT_QUAD_FLOATS;
                 }
-                const int key = RT_KEY(kind, idx), zero = 0;
-                std::memcpy(&r[0], &id, 4);
-                std::memcpy(&r[1], &key, 4);
-                std::memcpy(&r[2], &kind, 4);
-                std::memcpy(&r[3], &zero, 4);
-                std::memcpy(&r[4], src, (size_t)nf * sizeof(float));
+                // {key, record...} (rt_layout.h): kind = key & 3, the id
+                // follows from the index
+                const int key = RT_KEY(kind, idx);
+                std::memcpy(&r[0], &key, 4);
+                std::memcpy(&r[1], src, (size_t)nf * sizeof(float));
             }
         }
     }

@@ -427,54 +427,51 @@ __device__ __forceinline__ bool bvh_safe(const rt_kparams& K, f3 o, f3 d) {
     return pm < 1e37f && K.ovf_im * pm < 3e36f;
 }
 
-// Leaf record (rt_layout.h RT_LEAF_FLOATS): {id, key, kind, 0, record...};
-// the header and the first record float4 are loaded together (no dependent
-// index load in the leaf loop).
-__device__ __forceinline__ void leaf_test(const float* r, f3 o, f3 d, float a2, float a4, float& best_t, int& best_id,
-                                          int& best_key) {
-    const float4 h = *reinterpret_cast<const float4*>(r);
-    const float4 a = *reinterpret_cast<const float4*>(r + 4);
-    const int id = __float_as_int(h.x), key = __float_as_int(h.y), kind = __float_as_int(h.z);
+// Leaf record (rt_layout.h RT_LEAF_FLOATS) {key, record...}: kind = key & 3,
+// the primitive id follows from the index key >> 2 (no id / kind words: a
+// triangle's plane and first edge are its first 48 bytes, one load round
+// trip; config 5 89.8 -> 88.8 ms); each later edge loads only the 16-byte
+// pieces it still needs, so a lane whose point fails an edge requests no
+// further record bytes (the walk is bound by its L1 / L2 request traffic).
+__device__ __forceinline__ void leaf_test(const rt_kparams& K, const float* r, f3 o, f3 d, float a2, float a4,
+                                          float& best_t, int& best_id, int& best_key) {
+    const float4 c0 = *reinterpret_cast<const float4*>(r);      // key, n.xyz | key, c.xyz
+    const float4 c1 = *reinterpret_cast<const float4*>(r + 4);  // d, v0.xyz   | r^2
+    const int key = __float_as_int(c0.x), kind = key & 3, idx = key >> 2;
     if (kind == 0) {  // sphere {c, r^2}, Intersection.cuh:15-62
-        const f3 xp = mk(o.x - a.x, o.y - a.y, o.z - a.z);
+        const f3 xp = mk(o.x - c0.y, o.y - c0.z, o.z - c0.w);
         const float b = 2.0f * dot(xp, d);
-        const float c = dot(xp, xp) - a.w;
+        const float c = dot(xp, xp) - c1.x;
         const float disc = b * b - a4 * c;
         if (!(disc < 0.0f) && !(b >= 0.0f)) {
             const float t = (-b - sqrtf(disc)) / a2;
             if (key_accept(t, key, best_t, best_key)) {
                 best_t = t;
-                best_id = id;
+                best_id = idx;
                 best_key = key;
             }
         }
         return;
     }
-    const float* q = r + 4;  // triangle / quad record {n, d, (v_k, in_k)...}
-    // the first edge's record is loaded with the plane (one memory round
-    // trip less: config 5 91.8 -> 91.0 ms)
-    const float4 e0 = *reinterpret_cast<const float4*>(q + 4);   // v0.xyz in0.x
-    const float4 e1 = *reinterpret_cast<const float4*>(q + 8);   // in0.yz v1.xy
-    const float nd = a.x * d.x + a.y * d.y + a.z * d.z;
+    const float4 c2 = *reinterpret_cast<const float4*>(r + 8);  // in0.xyz, v1.x
+    const float nd = c0.y * d.x + c0.z * d.y + c0.w * d.z;
     if (fabsf(nd) < RT_NEAR_ZERO) return;
-    const float t = -((a.x * o.x + a.y * o.y + a.z * o.z) + a.w) / nd;
+    const float t = -((c0.y * o.x + c0.z * o.y + c0.w * o.z) + c1.x) / nd;
     if (!key_accept(t, key, best_t, best_key)) return;
     const f3 P = add(o, scale(t, d));
-    // the later edge tests in order, each loading only its own {v_k, in_k}:
-    // a lane whose point fails an edge requests no further record bytes (the
-    // walk is bound by its L1 / L2 request traffic); same tests, same result
-    if (dot(mk(e0.w, e1.x, e1.y), sub(P, mk(e0.x, e0.y, e0.z))) < 0.0f) return;
-    const float4 e2 = *reinterpret_cast<const float4*>(q + 12);  // v1.z in1.xyz
-    if (dot(mk(e2.y, e2.z, e2.w), sub(P, mk(e1.z, e1.w, e2.x))) < 0.0f) return;
-    const float4 e3 = *reinterpret_cast<const float4*>(q + 16);  // v2.xyz in2.x
-    const float4 e4 = *reinterpret_cast<const float4*>(q + 20);  // in2.yz (v3.xy)
-    if (dot(mk(e3.w, e4.x, e4.y), sub(P, mk(e3.x, e3.y, e3.z))) < 0.0f) return;
+    if (dot(mk(c2.x, c2.y, c2.z), sub(P, mk(c1.y, c1.z, c1.w))) < 0.0f) return;
+    const float4 c3 = *reinterpret_cast<const float4*>(r + 12);  // v1.yz, in1.xy
+    const float4 c4 = *reinterpret_cast<const float4*>(r + 16);  // in1.z, v2.xyz
+    if (dot(mk(c3.z, c3.w, c4.x), sub(P, mk(c2.w, c3.x, c3.y))) < 0.0f) return;
+    const float4 c5 = *reinterpret_cast<const float4*>(r + 20);  // in2.xyz, v3.x
+    if (dot(mk(c5.x, c5.y, c5.z), sub(P, mk(c4.y, c4.z, c4.w))) < 0.0f) return;
     if (kind == 3) {
-        const float4 e5 = *reinterpret_cast<const float4*>(q + 24);  // v3.z in3.xyz
-        if (dot(mk(e5.y, e5.z, e5.w), sub(P, mk(e4.z, e4.w, e5.x))) < 0.0f) return;
+        const float4 c6 = *reinterpret_cast<const float4*>(r + 24);  // v3.yz, in3.xy
+        const float4 c7 = *reinterpret_cast<const float4*>(r + 28);  // in3.z
+        if (dot(mk(c6.z, c6.w, c7.x), sub(P, mk(c5.w, c6.x, c6.y))) < 0.0f) return;
     }
     best_t = t;
-    best_id = id;
+    best_id = (kind == 2 ? K.n_sph + K.n_pln : K.n_sph + K.n_pln + K.n_tri) + idx;
     best_key = key;
 }
 
@@ -607,7 +604,7 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
             const int first = leaf & 0xffffff, count = leaf >> 24;
             for (int k = 0; k < count; k++) {
                 RT_BRANCH_COUNT(K, 6);
-                leaf_test(K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
+                leaf_test(K, K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
                           best_key);
             }
         }
@@ -1698,7 +1695,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 const int first = leaf & 0xffffff, count = leaf >> 24;
                 for (int k = 0; k < count; k++) {
                     RT_BRANCH_COUNT(K, 6);
-                    leaf_test(K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
+                    leaf_test(K, K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
                               best_key);
                 }
                 leaf = -1;
@@ -1706,7 +1703,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             if (leaf2 >= 0) {
                 const int first = leaf2 & 0xffffff, count = leaf2 >> 24;
                 for (int k = 0; k < count; k++)
-                    leaf_test(K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
+                    leaf_test(K, K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
                               best_key);
                 leaf2 = -1;
             }

@@ -35,7 +35,7 @@
 #define RT_QUAD_FLOATS 32
 #define RT_TRI_CULL 24   // offset of the cull sphere in a triangle record
 #define RT_QUAD_CULL 28
-#define RT_LEAF_FLOATS 32  // BVH leaf record: 4 header + the record without its cull sphere (<= 28 floats)
+#define RT_LEAF_FLOATS 32  // BVH leaf record: RT_KEY + the record without its cull sphere (<= 28 floats)
 #ifndef RT_HIT_FLOATS
 #define RT_HIT_FLOATS 16
 #endif
@@ -73,8 +73,9 @@ struct rt_kparams {
     // floats {bmin.xyz, miss, bmax.xyz, leaf}, depth-first (first child =
     // node + 1, near side of the split first for that octant), miss = next node when
     // the subtree is skipped (-1 = done), leaf = -1 (internal) or
-    // (count << 24) | first index into bvh_leafrec: {id, RT_KEY, kind (0
-    // sphere, 2 triangle, 3 quad), 0, then the compiled record}.
+    // (count << 24) | first index into bvh_leafrec: {RT_KEY (kind = key & 3:
+    // 0 sphere, 2 triangle, 3 quad; index = key >> 2), then the compiled
+    // record without its cull sphere}.
     const float* bvh_nodes;
     const float* bvh_leafrec;   // leaf records in leaf order, RT_LEAF_FLOATS each
     int bvh_order_stride;
