@@ -97,6 +97,27 @@ def test_stress_c5_rows_bvh(gpu, oracle, monkeypatch, n16, mask):
     same_state(gpu, st)
 
 
+@pytest.mark.parametrize("batch,refill", [(1, 1), (64, 64), (33, 1), (1, 64), (60, 36)])
+def test_stress_bvh_refill_schedules(bwrt_lib, oracle, monkeypatch, batch, refill):
+    """The refill kernel's scheduling knobs only decide WHEN a lane tests its
+    parked leaves (BWRT_LEAF_BATCH: once that many of 64 lanes are ready) and
+    takes its next ray (BWRT_REFILL: once that many of 64 have finished), never
+    what it tests: every schedule, from one lane at a time to whole waves,
+    is bit-exact with the oracle (8 bounces, the stress scene's BVH)."""
+    from bwrt import Renderer
+    monkeypatch.setenv("BWRT_LEAF_BATCH", str(batch))
+    monkeypatch.setenv("BWRT_REFILL", str(refill))
+    r = Renderer(0, lib=bwrt_lib)  # the knobs are read when the context is made
+    monkeypatch.delenv("BWRT_LEAF_BATCH")
+    monkeypatch.delenv("BWRT_REFILL")
+    try:
+        img, st = run_pair(r, oracle, scenes.stress_scene(), 96, 54, 2, 8)
+        assert np.array_equal(img, st.rgba)
+        same_state(r, st)
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("k,n16,mb", [(3e4, 0, 6), (1e-4, 1, 6), (1.0, 1, 6), (100.0, 1, 1), (1e3, 1, 6), (1e10, 0, 3)])
 def test_stress_bvh_scaled(gpu, oracle, monkeypatch, capfd, k, n16, mb):
     """The stress scene scaled by 3e4 (box corners beyond the fp16 range:
