@@ -677,7 +677,7 @@ def test_launch_order_feedback(bwrt_lib, oracle, monkeypatch, scene_name, w, h, 
         _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
     try:
         r.set_scene(scene)
-        for _ in range(3):
+        for _ in range(4):  # blockIdx order first, then each launch in the order sorted from the last
             r.init_rand(w, h)
             img = r.render(w, h, spp, mb, first_frame=1)
             assert np.array_equal(img, st.rgba)
