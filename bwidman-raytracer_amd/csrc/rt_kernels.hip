@@ -330,6 +330,9 @@ __device__ __forceinline__ void polygon_test(const rt_kparams& K, const __attrib
 typedef const __attribute__((address_space(4))) float* cfloat_ptr;
 __device__ __forceinline__ cfloat_ptr as_const(const float* p) { return (cfloat_ptr)p; }
 
+// QUADS = false: the scene has no quads (launch policy); the quad tests are
+// compiled out, which shortens the loop body (config 3: 0.871 -> 0.865 ms)
+template <bool QUADS = true>
 __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
     const float a = dot(d, d);
     const float a4 = 4.0f * a;
@@ -372,7 +375,7 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
             }
         }
         if (i < K.n_tri) polygon_test(K, as_const(K.tri) + RT_TRI_FLOATS * i, 3, o, d, tri_base + i, cr, best_t, best_id);
-        if (i < K.n_quad)
+        if (QUADS && i < K.n_quad)
             polygon_test(K, as_const(K.quad) + RT_QUAD_FLOATS * i, 4, o, d, quad_base + i, cr, best_t, best_id);
     }
 }
@@ -611,12 +614,12 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
     }
 }
 
-template <bool BVH>
+template <bool BVH, bool QUADS = true>
 __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
     if (BVH)
         closest_hit_bvh(K, o, d, best_t, best_id);
     else
-        closest_hit_brute(K, o, d, best_t, best_id);
+        closest_hit_brute<QUADS>(K, o, d, best_t, best_id);
 }
 
 __device__ __forceinline__ unsigned to_u8(float v) {
@@ -1086,7 +1089,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 //
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
-template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false>
+template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC && !BVH ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
     enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
@@ -1394,7 +1397,7 @@ rt_render_sorted_kernel(rt_kparams K) {
             has_ray = false;
             float t;
             int id;
-            closest_hit<BVH>(K, o, d, t, id);
+            closest_hit<BVH, QUADS>(K, o, d, t, id);
             if (id >= 0) {
                 const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
                 hP = add(o, scale(t, d));
@@ -1787,12 +1790,20 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     } else if (K.order_n != grid) {
         K.group_order = nullptr;  // no order for this grid yet: blockIdx order
     }
-    if (SORTED && feedback)
+    // brute-force scenes without quads: the quad tests compiled out
+    const bool quads = BVH || K.n_quad > 0;
+    if (SORTED && feedback && quads)
         hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, true>), dim3((unsigned)grid), dim3(BLOCK),
                            lds, stream, K);
-    else if (SORTED)
+    else if (SORTED && feedback)
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, true, false>), dim3((unsigned)grid),
+                           dim3(BLOCK), lds, stream, K);
+    else if (SORTED && quads)
         hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC>), dim3((unsigned)grid), dim3(BLOCK), lds,
                            stream, K);
+    else if (SORTED)
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, false, false>), dim3((unsigned)grid),
+                           dim3(BLOCK), lds, stream, K);
     else
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
     hipError_t e = hipGetLastError();
