@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rt_layout.h"
+#include "rt_sqrt.h"
 
 namespace {
 
@@ -57,8 +58,9 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     float k = a.x * b.y - a.y * b.x;
     return mk(i, j, k);
 }
-__device__ __forceinline__ float length3(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
-__device__ __forceinline__ f3 normalize3(f3 v) { return scale(1.0f / length3(v), v); }
+__device__ __forceinline__ float length3(f3 v) { return sqrt_cr(v.x * v.x + v.y * v.y + v.z * v.z); }
+// scale(1 / length(v), v) (Math.cuh normalize): inv_length_cr = RN(1 / RN(sqrt))
+__device__ __forceinline__ f3 normalize3(f3 v) { return scale(inv_length_cr(v.x * v.x + v.y * v.y + v.z * v.z), v); }
 __device__ __forceinline__ float square(float x) { return x * x; }
 __device__ __forceinline__ float chi(float x) { return (x > 0.0f) ? 1.0f : 0.0f; }
 
@@ -162,7 +164,7 @@ __device__ __forceinline__ float atan_nn(float x) {  // orc_atanf
     float y;
     if (x > 2.414213562373095f) {
         y = 1.5707963267948966f;
-        x = -(1.0f / x);
+        x = -rcp_cr(x);
     } else if (x > 0.4142135623730950f) {
         y = 0.7853981633974483f;
         x = (x - 1.0f) / (x + 1.0f);
@@ -188,8 +190,8 @@ __device__ __forceinline__ float atan_nn(float x) {  // orc_atanf
 // roughness * roughness * tanTheta * tanTheta left to right, Main.cu:119)
 __device__ __forceinline__ float shadowing_masking(f3 dir, f3 n, f3 m, float rough2) {
     float vdn = dot(dir, n);
-    float tan_theta = fmaxf(1.0f / (vdn * vdn) - 1.0f, 0.0f);
-    return chi(dot(dir, m) / vdn) * 2.0f / (1.0f + sqrtf(1.0f + rough2 * tan_theta * tan_theta));
+    float tan_theta = fmaxf(rcp_cr(vdn * vdn) - 1.0f, 0.0f);
+    return chi(dot(dir, m) / vdn) * 2.0f / (1.0f + sqrt_cr(1.0f + rough2 * tan_theta * tan_theta));
 }
 
 // fresnel(i, m, 1, ior) with ior2m1 = ior*ior/(1*1) - 1 precomputed
@@ -197,7 +199,7 @@ __device__ __forceinline__ float fresnel(f3 incident, f3 normal, float ior2m1) {
     float c = fabsf(dot(incident, normal));
     float g_root = ior2m1 + c * c;
     if (g_root < 0.0f) return 1.0f;
-    float g = sqrtf(g_root);
+    float g = sqrt_cr(g_root);
     return 0.5f * square(g - c) / square(g + c) *
            (1.0f + square(c * (g + c) - 1.0f) / square(c * (g - c) + 1.0f));
 }
@@ -358,7 +360,7 @@ __device__ __forceinline__ void closest_hit_brute(const rt_kparams& K, f3 o, f3 
             // i.e. t <= 0 <= nearZero, rejected by the reference as well
             if (!(disc < 0.0f) && !(b >= 0.0f && disc == disc && a2 > 0.0f)) {
                 RT_BRANCH_COUNT(K, 0);
-                float t = (-b - sqrtf(disc)) / a2;
+                float t = (-b - sqrt_cr(disc)) / a2;
                 if (!(t <= RT_NEAR_ZERO || t > best_t)) {
                     best_t = t;
                     best_id = i;
@@ -450,7 +452,7 @@ __device__ __forceinline__ void leaf_test(const rt_kparams& K, const float* r, f
         const float c = dot(xp, xp) - c1.x;
         const float disc = b * b - a4 * c;
         if (!(disc < 0.0f) && !(b >= 0.0f)) {
-            const float t = (-b - sqrtf(disc)) / a2;
+            const float t = (-b - sqrt_cr(disc)) / a2;
             if (key_accept(t, key, best_t, best_key)) {
                 best_t = t;
                 best_id = idx;
@@ -491,7 +493,7 @@ __device__ __forceinline__ void prim_test(const rt_kparams& K, int id, f3 o, f3 
         const float c = dot(xp, xp) - s.w;
         const float disc = b * b - a4 * c;
         if (!(disc < 0.0f) && !(b >= 0.0f)) {
-            const float t = (-b - sqrtf(disc)) / a2;
+            const float t = (-b - sqrt_cr(disc)) / a2;
             const int key = RT_KEY(0, id);
             if (key_accept(t, key, best_t, best_key)) {
                 best_t = t;
@@ -560,7 +562,7 @@ __device__ __forceinline__ void closest_hit_bvh(const rt_kparams& K, f3 o, f3 d,
     const float tiny = 1e-20f;
     const f3 dc = mk(fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x, fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y,
                      fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z);
-    const f3 inv = mk(1.0f / dc.x, 1.0f / dc.y, 1.0f / dc.z);
+    const f3 inv = mk(rcp_cr(dc.x), rcp_cr(dc.y), rcp_cr(dc.z));
     // slab distances as fma(b, inv, -o*inv): the rounding of o*inv (at most
     // 2^-24 |o*inv| per axis) is covered by the absolute margin `m`
     const f3 oinv = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
@@ -645,7 +647,7 @@ __device__ __forceinline__ unsigned tone_map(float ax, float ay, float az, unsig
         float num = cc * (2.51f * cc + 0.03f);
         float den = cc * (2.43f * cc + 0.59f) + 0.14f;
         float tm = fminf(num / den, 1.0f);  // clamp(color, 1.0f): upper only
-        float g = sqrtf(tm) * 255.0f;
+        float g = sqrt_cr(tm) * 255.0f;
         px |= to_u8(g) << (8 * ch);
     }
     return px;
@@ -744,7 +746,7 @@ __device__ __forceinline__ f3 specular_scatter(Xorwow& rs, f3 d, f3 n, float rou
                                                float ior2m1, float& kspec) {
     const float e1 = rand_range(rs, 1.0f);
     const float e2 = rand_range(rs, 1.0f);
-    const float theta = atan_nn(rough * sqrtf(e1) / sqrtf(1.0f - e1));
+    const float theta = atan_nn(rough * sqrt_cr(e1) / sqrt_cr(1.0f - e1));
     const float phi = 2.0f * RT_PI * e2;
     float st, ct, sp, cp;
     sincos_nn(theta, st, ct);
@@ -922,7 +924,7 @@ rt_render_kernel(rt_kparams K) {
                     // genMicrofacetNormal (Main.cu:170-185)
                     const float e1 = rand_range(px.rs, 1.0f);
                     const float e2 = rand_range(px.rs, 1.0f);
-                    const float theta = atan_nn(rough * sqrtf(e1) / sqrtf(1.0f - e1));
+                    const float theta = atan_nn(rough * sqrt_cr(e1) / sqrt_cr(1.0f - e1));
                     const float phi = 2.0f * RT_PI * e2;
                     float st, ct, sp, cp;
                     sincos_nn(theta, st, ct);
@@ -1638,7 +1640,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             const f3 dc = mk(fabsf(d.x) < tiny ? copysignf(tiny, d.x) : d.x,
                              fabsf(d.y) < tiny ? copysignf(tiny, d.y) : d.y,
                              fabsf(d.z) < tiny ? copysignf(tiny, d.z) : d.z);
-            inv = mk(1.0f / dc.x, 1.0f / dc.y, 1.0f / dc.z);
+            inv = mk(rcp_cr(dc.x), rcp_cr(dc.y), rcp_cr(dc.z));
             oinv = mk(o.x * inv.x, o.y * inv.y, o.z * inv.z);
             m = 1e-6f + 9.5367431640625e-07f * fmaxf(fmaxf(fabsf(oinv.x), fabsf(oinv.y)), fabsf(oinv.z));
             const int order = ((d.x < 0.0f) | ((d.y < 0.0f) << 1) | ((d.z < 0.0f) << 2)) & K.bvh_order_mask;

@@ -1,6 +1,11 @@
+#!/bin/bash
+# one GPU A/B session: parity subset for the candidate variant, then
+# alternating c3 / c4 bench runs (variants from tools/variants.sh)
 set -o pipefail
 V=$PWD/bwidman-raytracer_amd/build/variants
+CAND=${CAND:-sq}; BASE=${BASE:-bop}
 mkdir -p gpurun_out
-BWRT_LIB=$V/bop/libbwrt.so timeout -k 10 300 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread -k "config3 or random or small or stress_c5" > gpurun_out/ab1_pt.log 2>&1; rc=$?; tail -1 gpurun_out/ab1_pt.log; [ $rc = 0 ] || exit 1
-timeout -k 10 600 tools/ab_libs.sh 5 old bop || exit 1
-BENCH_ARGS="--config c4 --steps 5 --warmup 2" timeout -k 10 300 tools/ab_libs.sh 2 old bop
+timeout -k 10 120 build/sqrtx || exit 1
+BWRT_LIB=$V/$CAND/libbwrt.so timeout -k 10 300 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread -k "config3 or random or small or stress_c5" > gpurun_out/ab_pt.log 2>&1; rc=$?; tail -1 gpurun_out/ab_pt.log; [ $rc = 0 ] || exit 1
+timeout -k 10 600 tools/ab_libs.sh 5 $BASE $CAND || exit 1
+BENCH_ARGS="--config c4 --steps 5 --warmup 2" timeout -k 10 300 tools/ab_libs.sh 2 $BASE $CAND
