@@ -1097,7 +1097,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC && !BVH ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
-    enum { M_IDLE = 0, M_REGEN = 1, M_SHADE = 2 };
+    // a lane's next task: none (idle), camera ray, diffuse or specular bounce
     enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
@@ -1154,12 +1154,12 @@ rt_render_sorted_kernel(rt_kparams K) {
     if (ORDER && tid == 0) K.group_cost[group] = (unsigned)__builtin_amdgcn_s_memrealtime();
     PixelState px;
     load_item(K, npix, nitems, group * BLOCK + tid, px);
-    int mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
+    int mode = px.passes_left > 0 ? T_REGEN : T_NONE;
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
-    f3 hP = o, hn = o;  // pending hit: point, normal
+    f3 hn = o;  // pending hit's normal (its point is o)
     int hid = 0, depth = 0;
-    bool hspec = false, has_ray = false;
+    bool has_ray = false;
     int parity = 0;
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
 
@@ -1187,7 +1187,7 @@ rt_render_sorted_kernel(rt_kparams K) {
         // one pixel per lane (the grid covers every work item): a finished
         // pixel is stored after the loop, by the whole wave at once, and the
         // camera set-up constants are not live inside the loop
-        mode = px.passes_left > 0 ? M_REGEN : M_IDLE;
+        mode = px.passes_left > 0 ? T_REGEN : T_NONE;
     };
     bool ended = false;  // path ended this round: finish_path() once, after the I-phase
 
@@ -1219,7 +1219,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     } while (0)
 #endif
     while (true) {
-        const int task = mode == M_REGEN ? T_REGEN : (mode == M_SHADE ? (hspec ? T_SPEC : T_DIFF) : T_NONE);
+        const int task = mode;
         STAMP(7);
         // every owner has read its previous task result out of the slots
         // before any wave overwrites them with this round's tasks
@@ -1343,26 +1343,26 @@ rt_render_sorted_kernel(rt_kparams K) {
         }
         parity ^= 1;
 
-        // ---- owner: take the task result back
+        // ---- owner: take the task result back.  The result direction goes
+        // straight into d and the pending hit point already is o (I-phase),
+        // so no ray registers are copied here
         if (slot >= 0) {
-            const f3 r = mk(RES(0, slot), RES(1, slot), RES(2, slot));
+            d = mk(RES(0, slot), RES(1, slot), RES(2, slot));
             px.rs.d = __float_as_uint(RES(4, slot));
             px.rs.v0 = __float_as_uint(RES(5, slot));
             px.rs.v1 = __float_as_uint(RES(6, slot));
             px.rs.v2 = __float_as_uint(RES(7, slot));
             px.rs.v3 = __float_as_uint(RES(8, slot));
             px.rs.v4 = __float_as_uint(RES(9, slot));
-            {
-            mode = M_IDLE;
+            mode = T_NONE;
             if (task == T_REGEN) {
                 o = cam;
-                d = r;
                 depth = 0;
                 has_ray = true;
             } else {
                 const int code = task == T_SPEC ? ~hid : hid;
                 const float kspec = task == T_SPEC ? RES(3, slot) : 0.0f;
-                const float cosang = dot(r, hn);  // cosAngle, Main.cu:264
+                const float cosang = dot(d, hn);  // cosAngle, Main.cu:264
                 if (depth < K.max_bounces) {
                     if (!GREC || depth < LL) {
                         rec_code[depth * BLOCK] = code;
@@ -1373,9 +1373,7 @@ rt_render_sorted_kernel(rt_kparams K) {
                         grec_k[(depth - LL) * RS] = kspec;
                         grec_c[(depth - LL) * RS] = cosang;
                     }
-                    o = hP;
-                    d = r;
-                    has_ray = true;
+                    has_ray = true;  // from the hit point o along d
                 } else {  // next query would exceed maxBounces (Main.cu:210): the path ends
                     SLOT(4, slot) = kspec;
                     SLOT(5, slot) = cosang;
@@ -1383,7 +1381,6 @@ rt_render_sorted_kernel(rt_kparams K) {
                     ended = true;
                 }
                 depth++;
-            }
             }
         }
 
@@ -1405,12 +1402,12 @@ rt_render_sorted_kernel(rt_kparams K) {
             closest_hit<BVH, QUADS>(K, o, d, t, id);
             if (id >= 0) {
                 const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
-                hP = add(o, scale(t, d));
+                o = add(o, scale(t, d));  // the hit point: the next ray's origin
                 hn = mk(h0.x, h0.y, h0.z);
-                if (h0.w != 0.0f) hn = normalize3(sub(hP, hn));  // sphere normal
+                if (h0.w != 0.0f) hn = normalize3(sub(o, hn));  // sphere normal
                 hid = id;
-                hspec = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE;
-                mode = M_SHADE;
+                // brdfChoice (Main.cu:243): specular or diffuse bounce next round
+                mode = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE ? T_SPEC : T_DIFF;
             } else {
                 ended = true;
             }

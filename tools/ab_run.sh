@@ -6,6 +6,6 @@ V=$PWD/bwidman-raytracer_amd/build/variants
 CAND=${CAND:-sq}; BASE=${BASE:-bop}
 mkdir -p gpurun_out
 timeout -k 10 120 build/sqrtx || exit 1
-BWRT_LIB=$V/$CAND/libbwrt.so timeout -k 10 300 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread -k "config3 or random or small or stress_c5" > gpurun_out/ab_pt.log 2>&1; rc=$?; tail -1 gpurun_out/ab_pt.log; [ $rc = 0 ] || exit 1
+BWRT_LIB=$V/$CAND/libbwrt.so timeout -k 10 300 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread ${SUBSET:+-k "$SUBSET"} > gpurun_out/ab_pt.log 2>&1; rc=$?; tail -1 gpurun_out/ab_pt.log; [ $rc = 0 ] || exit 1
 timeout -k 10 600 tools/ab_libs.sh 5 $BASE $CAND || exit 1
 BENCH_ARGS="--config c4 --steps 5 --warmup 2" timeout -k 10 300 tools/ab_libs.sh 2 $BASE $CAND
