@@ -69,3 +69,18 @@ def test_transcendental_accuracy(oracle, fn, ref, lo, hi, maxulp):
 def test_atan_of_infinity(oracle):
     assert abs(oracle.lib().orc_atanf(float("inf")) - np.pi / 2) < 1e-7
     assert oracle.lib().orc_atanf(0.0) == 0.0
+
+
+@pytest.mark.gpu
+def test_sqrt_rcp_helpers_exhaustive():
+    """csrc/rt_sqrt.h's short in-range paths (sqrt_cr, rcp_cr, inv_length_cr)
+    equal the compiler's correctly rounded sqrtf, 1/x and 1/sqrtf for every
+    one of the 2^32 float inputs (tools/sqrt_exhaustive.hip on the GPU,
+    built by __graft_entry__.build())."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "sqrtx")
+    assert os.path.exists(exe), "build/sqrtx missing: run __graft_entry__.build()"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(": 0 mismatches") == 3, r.stdout
