@@ -44,6 +44,11 @@ __device__ __forceinline__ float rcp_core(float x) {  // |x| in [2^-60, 2^60]
     return __builtin_fmaf(e2, r, q);
 }
 
+#ifdef RT_PLAIN_SQRT  // A/B builds: the compiler's full sequences
+__device__ __forceinline__ float sqrt_cr(float x) { return sqrtf(x); }
+__device__ __forceinline__ float rcp_cr(float x) { return 1.0f / x; }
+__device__ __forceinline__ float inv_length_cr(float s) { return 1.0f / sqrtf(s); }
+#else
 __device__ __forceinline__ float sqrt_cr(float x) {
     if (x >= 0x1p-96f && x <= 0x1.fffffep+127f) return sqrt_core(x);
     return sqrtf(x);
@@ -61,3 +66,4 @@ __device__ __forceinline__ float inv_length_cr(float s) {
     if (s >= 0x1p-96f && s <= 0x1p+118f) return rcp_core(sqrt_core(s));
     return 1.0f / sqrtf(s);
 }
+#endif
