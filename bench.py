@@ -15,6 +15,9 @@ ms/frame = ms_per_step.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
                   [--no-cpu-baseline] [--cpu-threads T]
+The CPU baseline is the library's scalar C++ fallback (rt_render_cpu) on
+every CPU of the process's affinity (or --cpu-threads), timed on rank 0 at
+N = 1 after the GPU steps, and checked bit-exact against the GPU.
 For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
 """
 from __future__ import annotations
@@ -72,25 +75,52 @@ SCENE_DATA = {
 }
 
 
-def cpu_baseline(scene_key, w, h, spp, mb, threads):
-    """The oracle (C restatement, OpenMP over rows) on the host cores: the
-    reported CPU baseline ("port"), never the measured product."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as O
-    O.build()
-    if threads <= 0:
-        threads = min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1))
+# CPU-baseline sample: a row shard (every k-th row) of the bench frame, so
+# the scalar fallback's run stays within seconds on the big configs
+CPU_SAMPLE_ROW_STRIDE = {"c1": 1, "c2": 1, "c3": 1, "c4": 4, "c5": 27}
+
+
+def cpu_quota():
+    """CPUs of this process's cgroup quota (cpu.max), or None if unlimited."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if quota == "max" else float(quota) / float(period)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(lib, config, scene_key, w, h, spp, mb, threads, gpu_renderer=None):
+    """The product's scalar C++ CPU fallback (rt_create_cpu / rt_render_cpu:
+    the kernels' per-ray arithmetic compiled for the host, one pixel per loop
+    iteration, std::thread pool) timed on the host cores — the reported CPU
+    baseline ("fallback"), never the measured product.  With gpu_renderer the
+    sample is also rendered on the GPU from the same seeds and compared."""
+    stride = CPU_SAMPLE_ROW_STRIDE.get(config, 1)
+    aff = lib.rt_cpu_threads()
+    threads = threads if threads > 0 else aff
     scene = scenes.SCENES[scene_key]()
-    st = O.OracleState(w, h)
-    O.render(scene, st, 1, mb, first_frame=1, threads=threads)  # warm (pages, threads)
-    st = O.OracleState(w, h)
-    t0 = time.perf_counter()
-    O.render(scene, st, spp, mb, first_frame=1, threads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": round(w * h * spp * mb / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
-            "kind": "port", "ms_per_frame": round(dt * 1e3, 2),
-            "sample": f"one full {w}x{h} {spp}-spp {mb}-bounce frame of scene {scene_key} "
-                      f"(oracle/oracle.c, OpenMP, {threads} threads)"}
+    with Renderer.cpu(threads, lib=lib) as c:
+        c.set_scene(scene)
+        c.init_rand(w, h, 0, stride)
+        c.render(w, h, 1, mb, first_frame=1, row_stride=stride)  # warm (pages, threads)
+        c.init_rand(w, h, 0, stride)
+        t0 = time.perf_counter()
+        img = c.render(w, h, spp, mb, first_frame=1, row_stride=stride)
+        dt = time.perf_counter() - t0
+    rows = img.shape[0]
+    out = {"value": round(rows * w * spp * mb / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
+           "kind": "fallback", "ms_per_sample": round(dt * 1e3, 2),
+           "sample": f"{'one full' if stride == 1 else f'rows y = 0 mod {stride} of one'} {w}x{h} {spp}-spp "
+                     f"{mb}-bounce frame of scene {scene_key} ({rows} rows; libbwrt.so rt_render_cpu, "
+                     f"{threads} threads; sched affinity {aff} CPUs, cgroup quota "
+                     f"{cpu_quota() or 'none'})"}
+    if stride == 1:
+        out["ms_per_frame"] = out["ms_per_sample"]
+    if gpu_renderer is not None:
+        gpu_renderer.init_rand(w, h, 0, stride)
+        g = gpu_renderer.render(w, h, spp, mb, first_frame=1, row_stride=stride)
+        out["bit_exact_vs_gpu"] = bool((g == img).all())
+    return out
 
 
 def load_traffic(path, workload_key):
@@ -257,7 +287,11 @@ def main():
                 "active_lanes_per_valu": round(v["active_lanes_per_valu"], 2),
                 "counters": traffic.get("source")}
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(scene_key, W, H, SPP, MB, args.cpu_threads)
+            torch.cuda.synchronize(dev)
+            with Renderer(dev_index, lib=lib) as check:
+                check.set_scene(scene)
+                out["cpu_baseline"] = cpu_baseline(lib, args.config, scene_key, W, H, SPP, MB, args.cpu_threads,
+                                                   gpu_renderer=check)
         print(json.dumps(out), flush=True)
     if args.verify:
         # one more sharded + gathered frame from freshly seeded RNG streams

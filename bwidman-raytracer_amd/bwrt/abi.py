@@ -5,7 +5,8 @@ The structs are byte-compatible with the reference's world types
 tests/test_abi.py pins every size and offset.
 
 Loading policy: the library is the product, so a missing or unloadable
-libbwrt.so raises immediately (there is no CPU fallback).  When PyTorch is
+libbwrt.so raises immediately.  Its scalar C++ CPU fallback (rt_create_cpu)
+lives in the same library and runs only when asked for explicitly.  When PyTorch is
 used in the same process (bench.py, multi-GPU), import torch BEFORE calling
 load(): libbwrt.so then binds to the HIP runtime torch already loaded
 (same soname libamdhip64.so.7), so device pointers and streams are shared.
@@ -79,6 +80,7 @@ class RenderParams(C.Structure):
 RT_OK = 0
 RT_ERR_INVALID_ARGUMENT = -1
 RT_ERR_NO_DEVICE = -2
+RT_ERR_UNSUPPORTED = -6
 RT_MAX_BOUNCES = 32
 RT_DEFAULT_MAX_BOUNCES = 5
 
@@ -94,12 +96,17 @@ def _proto(lib):
         "rt_device_count": (C.c_int, []),
         "rt_create": (C.c_int, [C.c_int, P(vp)]),
         "rt_destroy": (None, [vp]),
+        "rt_cpu_threads": (C.c_int, []),
+        "rt_create_cpu": (C.c_int, [C.c_int, P(vp)]),
+        "rt_context_threads": (C.c_int, [vp]),
+        "rt_render_cpu": (C.c_int, [vp, P(RenderParams), C.c_int, vp, vp]),
         "rt_set_scene": (C.c_int, [vp, P(SceneStruct)]),
         "rt_set_camera": (C.c_int, [vp, P(Camera)]),
         "rt_reset_accumulation": (C.c_int, [vp]),
         "rt_frame_counter": (C.c_uint, [vp]),
         "rt_set_max_bounces": (C.c_int, [vp, C.c_int]),
         "rt_set_background": (C.c_int, [vp, C.c_float, C.c_float, C.c_float]),
+        "rt_set_samples_per_pixel": (C.c_int, [vp, C.c_int]),
         "rt_get_camera": (C.c_int, [vp, P(Camera)]),
         "rt_apply_controls": (C.c_int, [P(Camera), C.c_uint, C.c_float]),
         "rt_controls": (C.c_int, [vp, C.c_uint, C.c_float]),
@@ -141,7 +148,7 @@ def load(path: str | None = None):
     if not os.path.exists(p):
         raise RuntimeError(
             f"libbwrt.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
-            " (the HIP library is the product; there is no CPU fallback)")
+            " (the HIP library is the product; nothing runs without it)")
     lib = _proto(C.CDLL(p))
     if path is None:
         _lib = lib

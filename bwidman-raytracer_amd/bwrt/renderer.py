@@ -4,7 +4,10 @@ Mirrors /root/reference/bwidman-raytracer/src/Main.cu: allocateScene()
 (:38-109) -> Renderer.set_scene(); the frame loop's render() +
 accumulatedFrames++ (:467-480) -> Renderer.render(); controls()' reset
 (Controls.cuh:15..69) -> Renderer.reset_accumulation() / set_camera().
-Every call goes to libbwrt.so (HIP); there is no CPU path.
+Every call goes to libbwrt.so: Renderer(device) renders with the HIP
+kernels; Renderer.cpu(threads) makes a context of the library's scalar C++
+CPU fallback (rt_create_cpu, the same per-ray arithmetic, bit-identical
+results).  A GPU renderer never falls back to the CPU.
 """
 from __future__ import annotations
 
@@ -16,12 +19,30 @@ from . import abi
 
 
 class Renderer:
-    def __init__(self, device: int = 0, lib=None):
+    def __init__(self, device: int = 0, lib=None, _cpu_threads=None):
         self.lib = lib or abi.load()
         self.ctx = C.c_void_p()
-        abi.check(self.lib, self.lib.rt_create(device, C.byref(self.ctx)))
-        self.device = device
+        if _cpu_threads is None:
+            abi.check(self.lib, self.lib.rt_create(device, C.byref(self.ctx)))
+        else:
+            abi.check(self.lib, self.lib.rt_create_cpu(_cpu_threads, C.byref(self.ctx)))
+        self.device = device if _cpu_threads is None else -1
         self.scene = None
+
+    @classmethod
+    def cpu(cls, threads: int = 0, lib=None) -> "Renderer":
+        """A context of the scalar C++ CPU fallback on `threads` host threads
+        (0 = every CPU this process may run on)."""
+        return cls(-1, lib=lib, _cpu_threads=threads)
+
+    @property
+    def is_cpu(self) -> bool:
+        return self.device < 0
+
+    @property
+    def threads(self) -> int:
+        """Host threads of a CPU renderer (0 for a GPU one)."""
+        return self.lib.rt_context_threads(self.ctx)
 
     # -- context lifetime -------------------------------------------------
     def close(self):
@@ -66,6 +87,11 @@ class Renderer:
         """backgroundColor (Main.cu:27): radiance of misses and the depth cut-off."""
         self._check(self.lib.rt_set_background(self.ctx, r, g, b))
 
+    def set_samples_per_pixel(self, n: int):
+        """samplesPerPixel (Main.cu:27, 296-299): n paths per frame from one
+        jittered camera ray, the last one kept and scaled by 1/n (default 1)."""
+        self._check(self.lib.rt_set_samples_per_pixel(self.ctx, n))
+
     def get_camera(self):
         from .abi import Camera
         cam = Camera()
@@ -107,6 +133,17 @@ class Renderer:
         p = self.params(width, height, samples, max_bounces, first_frame, row_offset, row_stride)
         self._check(self.lib.rt_render_ex(self.ctx, C.byref(p), out.ctypes.data,
                                           acc.ctypes.data if acc is not None else None))
+        return (out, acc) if want_accum else out
+
+    def render_cpu(self, width, height, samples, max_bounces=abi.RT_DEFAULT_MAX_BOUNCES, first_frame=0,
+                   row_offset=0, row_stride=1, threads=0, want_accum=False):
+        """rt_render_cpu: render() on a CPU renderer with this call's thread count."""
+        rows = self.lib.rt_shard_rows(height, row_offset, row_stride)
+        out = np.empty((rows, width, 4), dtype=np.uint8)
+        acc = np.empty((rows, width, 3), dtype=np.float32) if want_accum else None
+        p = self.params(width, height, samples, max_bounces, first_frame, row_offset, row_stride)
+        self._check(self.lib.rt_render_cpu(self.ctx, C.byref(p), threads, out.ctypes.data,
+                                           acc.ctypes.data if acc is not None else None))
         return (out, acc) if want_accum else out
 
     def render_device(self, params: abi.RenderParams, rgba_ptr: int, stream_ptr: int | None = None):

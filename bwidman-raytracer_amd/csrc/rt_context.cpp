@@ -11,13 +11,17 @@
 // the reference's order, so the kernel sees bit-identical inputs.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_abi.h"
@@ -32,6 +36,10 @@ hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offse
 extern thread_local long rt_order_groups_last;
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
                                   int shards, int rows_per_shard, hipStream_t stream);
+// scalar C++ CPU fallback (rt_cpu.cpp)
+int rt_cpu_render(const rt_kparams& K, int threads);
+void rt_cpu_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride);
+bool rt_cpu_supported();
 
 static_assert(sizeof(rt_vec3) == 12, "vec3d layout (Math.cuh:35-39)");
 static_assert(sizeof(rt_material) == 24, "material layout (WorldTypes.cuh:15-20)");
@@ -75,12 +83,25 @@ struct rt_context {
     bool bvh_refill = true;  // BWRT_BVH_REFILL=0: BVH scenes through the sorted kernel instead
     int grid_mult = 0;  // persistent grid = grid_mult x resident workgroups per CU x CUs
     hipStream_t stream = nullptr;
-    hipStream_t last_stream = nullptr;  // stream of the last launch (a caller's, via rt_render_device)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    // end of the last render launch on `render_stream`: a launch on another
-    // stream waits for it (the kernels read and write the same shard state)
+    // end of the last render launch (on `render_stream`, possibly a caller's
+    // stream): a launch on another stream waits for it, and host-side state
+    // writes wait for it (the kernels read and write the same shard state).
+    // Events, not stream handles, so a caller may destroy its streams.
     hipEvent_t ev_render = nullptr;
     hipStream_t render_stream = nullptr;
+    bool render_recorded = false;
+    // end of the last de-interleave on a caller's stream (rt_synchronize)
+    hipEvent_t ev_aux = nullptr;
+    bool aux_recorded = false;
+    // CPU backend (rt_create_cpu): host copies instead of device buffers, the
+    // scalar fallback of rt_cpu.cpp instead of the kernels
+    bool cpu = false;
+    int threads = 1;
+    float cpu_ms = -1.0f;
+    std::vector<float> scene_h;
+    std::vector<unsigned> rng_h, rgba_h;
+    std::vector<float> accum_h;
     bool timed = false;
     std::string err;
 
@@ -117,6 +138,7 @@ struct rt_context {
     int refill = -1;             // BWRT_REFILL: BVH refill kernel refill threshold (-1 = launch policy)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
+    int spp_inner = 1;  // samplesPerPixel, Main.cu:27
 };
 
 namespace {
@@ -152,13 +174,12 @@ void free_buf(DevBuf& b) {
 
 // Host-side writes of context state (scene, RNG seeds, frameSum, checkpoint
 // restore) and buffer reallocation must not overlap a render still running
-// on a caller's stream (rt_render_device): wait for that stream first.
-// Work on c->stream is already ordered by the stream itself.
+// on a caller's stream (rt_render_device): wait for the last render launch
+// (its event, recorded on whatever stream it ran on).  Work on c->stream is
+// already ordered by the stream itself.
 int quiesce(rt_context* c) {
-    if (c->last_stream && c->last_stream != c->stream) {
-        HIP_TRY(c, hipStreamSynchronize(c->last_stream));
-        c->last_stream = c->stream;
-    }
+    if (c->cpu || !c->render_recorded) return RT_OK;
+    HIP_TRY(c, hipEventSynchronize(c->ev_render));
     return RT_OK;
 }
 
@@ -814,11 +835,11 @@ int rt_create(int device, rt_context** out) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_render, hipEventDisableTiming) != hipSuccess) {
-        delete c;
+        hipEventCreateWithFlags(&c->ev_render, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_aux, hipEventDisableTiming) != hipSuccess) {
+        rt_destroy(c);
         return RT_ERR_HIP;
     }
-    c->last_stream = c->stream;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = prop.multiProcessorCount;
@@ -838,11 +859,42 @@ int rt_create(int device, rt_context** out) {
     return RT_OK;
 }
 
+int rt_create_cpu(int threads, rt_context** out) {
+    if (!out) return RT_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (threads < 0) return RT_ERR_INVALID_ARGUMENT;
+    // rt_cpu.cpp is built for x86-64-v3 (hardware fma for the exactly
+    // specified fma steps of rt_path.h)
+    if (!rt_cpu_supported()) return RT_ERR_UNSUPPORTED;
+    rt_context* c = new rt_context();
+    c->cpu = true;
+    c->device = -1;
+    c->threads = threads > 0 ? threads : rt_cpu_threads();
+    *out = c;
+    return RT_OK;
+}
+
+int rt_cpu_threads(void) {
+    // the CPUs this process may run on (sched affinity), not the machine's
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) {
+        const int n = CPU_COUNT(&set);
+        if (n > 0) return n;
+    }
+    const unsigned n = std::thread::hardware_concurrency();
+    return n > 0 ? (int)n : 1;
+}
+
 void rt_destroy(rt_context* c) {
     if (!c) return;
+    if (c->cpu) {
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->last_stream && c->last_stream != c->stream) (void)hipStreamSynchronize(c->last_stream);
+    if (c->render_recorded) (void)hipEventSynchronize(c->ev_render);
+    if (c->aux_recorded) (void)hipEventSynchronize(c->ev_aux);
     free_buf(c->scene_buf);
     free_buf(c->rng);
     free_buf(c->accum);
@@ -854,6 +906,7 @@ void rt_destroy(rt_context* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev_render) (void)hipEventDestroy(c->ev_render);
+    if (c->ev_aux) (void)hipEventDestroy(c->ev_aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -865,7 +918,7 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     if ((s->sphere_count && !s->spheres) || (s->plane_count && !s->planes) ||
         (s->triangle_count && !s->triangles) || (s->quad_count && !s->quads))
         return fail(c, RT_ERR_INVALID_ARGUMENT, "null primitive array with non-zero count");
-    HIP_TRY(c, hipSetDevice(c->device));
+    if (!c->cpu) HIP_TRY(c, hipSetDevice(c->device));
     const int ns = s->sphere_count, np = s->plane_count, nt = s->triangle_count, nq = s->quad_count;
     const size_t off_pln = (size_t)ns * RT_SPH_FLOATS;
     const size_t off_tri = off_pln + (size_t)np * RT_PLN_FLOATS;
@@ -1128,12 +1181,16 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             }
         }
     }
-    const size_t bytes = h.size() * sizeof(float);
-    int rc = quiesce(c);  // a render on a caller's stream may still read the scene
-    if (!rc) rc = ensure_buf(c, c->scene_buf, bytes);
-    if (rc) return rc;
-    HIP_TRY(c, hipMemcpyAsync(c->scene_buf.p, h.data(), bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->cpu) {
+        c->scene_h.swap(h);
+    } else {
+        const size_t bytes = h.size() * sizeof(float);
+        int rc = quiesce(c);  // a render on a caller's stream may still read the scene
+        if (!rc) rc = ensure_buf(c, c->scene_buf, bytes);
+        if (rc) return rc;
+        HIP_TRY(c, hipMemcpyAsync(c->scene_buf.p, h.data(), bytes, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
     c->n_sph = ns;
     c->n_pln = np;
     c->n_tri = nt;
@@ -1261,6 +1318,15 @@ int rt_set_max_bounces(rt_context* c, int mb) {
     return RT_OK;
 }
 
+int rt_set_samples_per_pixel(rt_context* c, int n) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    if (n < 1) return fail(c, RT_ERR_INVALID_ARGUMENT, "samples per pixel < 1");
+    if (n > RT_MAX_SAMPLES_PER_PIXEL)
+        return fail(c, RT_ERR_UNSUPPORTED, "samples per pixel > %d", RT_MAX_SAMPLES_PER_PIXEL);
+    c->spp_inner = n;
+    return RT_OK;
+}
+
 int rt_shard_rows(int height, int row_offset, int row_stride) {
     return shard_rows(height, row_offset, row_stride == 0 ? 1 : row_stride);
 }
@@ -1273,9 +1339,28 @@ int rt_init_rand(rt_context* c, int width, int height, int row_offset, int row_s
                     row_offset, row_stride);
     if ((long long)width * height > (1ll << 31))
         return fail(c, RT_ERR_UNSUPPORTED, "image larger than 2^31 pixels");
-    HIP_TRY(c, hipSetDevice(c->device));
     const int rows = shard_rows(height, row_offset, row_stride);
     const size_t npix = (size_t)rows * width;
+    if (c->cpu) {
+        try {
+            c->rng_h.assign(npix * 6, 0u);
+            c->accum_h.assign(npix * 3, 0.0f);
+            c->rgba_h.assign(npix, 0u);
+        } catch (...) {
+            return fail(c, RT_ERR_OUT_OF_MEMORY, "host state for %zu pixels", npix);
+        }
+        rt_cpu_init_rand(c->rng_h.data(), width, rows, row_offset, row_stride);
+    }
+    if (c->cpu) {
+        c->width = width;
+        c->height = height;
+        c->row_offset = row_offset;
+        c->row_stride = row_stride;
+        c->rows = rows;
+        c->frame = 1;
+        return RT_OK;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
     int rc = quiesce(c);  // a render on a caller's stream may still use the state
     if (!rc) rc = ensure_buf(c, c->rng, npix * 6 * sizeof(unsigned));
     if (!rc) rc = ensure_buf(c, c->accum, npix * 3 * sizeof(float));
@@ -1304,14 +1389,14 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     if (p->max_bounces > RT_MAX_BOUNCES)
         return fail(c, RT_ERR_UNSUPPORTED, "max_bounces %d > %d", p->max_bounces, RT_MAX_BOUNCES);
     if (c->width != p->width || c->height != p->height || c->row_offset != p->row_offset ||
-        c->row_stride != stride || !c->rng.p) {
+        c->row_stride != stride || (c->cpu ? c->rng_h.empty() : !c->rng.p)) {
         int rc = rt_init_rand(c, p->width, p->height, p->row_offset, stride);
         if (rc) return rc;
     }
     first = p->first_frame ? p->first_frame : c->frame;
     if ((unsigned long long)first + (unsigned)p->samples > 0xffffffffull)
         return fail(c, RT_ERR_INVALID_ARGUMENT, "frame counter overflow");
-    HIP_TRY(c, hipSetDevice(c->device));
+    if (!c->cpu) HIP_TRY(c, hipSetDevice(c->device));
 
     std::memset(&K, 0, sizeof K);
     K.width = p->width;
@@ -1353,7 +1438,7 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     if (c->n_tri > nmax) nmax = c->n_tri;
     if (c->n_quad > nmax) nmax = c->n_quad;
     K.n_max = nmax;
-    const float* base = (const float*)c->scene_buf.p;
+    const float* base = c->cpu ? c->scene_h.data() : (const float*)c->scene_buf.p;
     K.sph = base;
     K.pln = base + c->off_pln;
     K.tri = base + c->off_tri;
@@ -1367,8 +1452,28 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.ovf_nm = c->ovf_nm;
     K.ovf_im = c->ovf_im;
     K.cull_dmax = c->cull_dmax;
-    K.rng = (unsigned*)c->rng.p;
-    K.accum = (float*)c->accum.p;
+    K.spp_inner = c->spp_inner;
+    K.rng = c->cpu ? c->rng_h.data() : (unsigned*)c->rng.p;
+    K.accum = c->cpu ? c->accum_h.data() : (float*)c->accum.p;
+    return RT_OK;
+}
+
+// The CPU backend's render: rt_cpu.cpp over the host state, synchronous
+static int cpu_render(rt_context* c, const rt_render_params* p, int threads, uint8_t* rgba_out, float* accum_out) {
+    rt_kparams K;
+    unsigned first = 0;
+    int rc = prepare(c, p, K, first);
+    if (rc) return rc;
+    const size_t npix = (size_t)c->rows * c->width;
+    K.rgba = c->rgba_h.data();
+    const auto t0 = std::chrono::steady_clock::now();
+    rt_cpu_render(K, threads > 0 ? threads : c->threads);
+    c->cpu_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->frame = first + (unsigned)p->samples;  // Main.cu:480 accumulatedFrames++
+    if (rgba_out) std::memcpy(rgba_out, c->rgba_h.data(), npix * 4);
+    if (accum_out)
+        for (size_t i = 0; i < npix; i++)
+            for (int ch = 0; ch < 3; ch++) accum_out[3 * i + ch] = c->accum_h[ch * npix + i];
     return RT_OK;
 }
 
@@ -1451,13 +1556,14 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     HIP_TRY(c, hipEventRecord(c->ev1, s));
     HIP_TRY(c, hipEventRecord(c->ev_render, s));
     c->render_stream = s;
+    c->render_recorded = true;
     c->timed = true;
-    c->last_stream = s;
     c->frame = first + (unsigned)samples;  // Main.cu:480 accumulatedFrames++
     return RT_OK;
 }
 
 int rt_render_ex(rt_context* c, const rt_render_params* p, uint8_t* rgba_out, float* accum_out) {
+    if (c && c->cpu) return cpu_render(c, p, 0, rgba_out, accum_out);
     rt_kparams K;
     unsigned first = 0;
     int rc = prepare(c, p, K, first);
@@ -1502,6 +1608,7 @@ int rt_render_multi(rt_context* const* ctxs, int n, int width, int height, int s
     if (!ctxs || n <= 0 || width <= 0 || height <= 0 || samples <= 0) return RT_ERR_INVALID_ARGUMENT;
     for (int i = 0; i < n; i++) {
         if (!ctxs[i]) return RT_ERR_INVALID_ARGUMENT;
+        if (ctxs[i]->cpu) return fail(ctxs[i], RT_ERR_UNSUPPORTED, "rt_render_multi: CPU context");
         for (int j = 0; j < i; j++)
             if (ctxs[j] == ctxs[i]) return fail(ctxs[i], RT_ERR_INVALID_ARGUMENT, "context listed twice");
     }
@@ -1563,6 +1670,7 @@ int rt_render_multi(rt_context* const* ctxs, int n, int width, int height, int s
 }
 
 int rt_render_device(rt_context* c, const rt_render_params* p, void* rgba_device, void* stream) {
+    if (c && c->cpu) return fail(c, RT_ERR_UNSUPPORTED, "rt_render_device: CPU context");
     rt_kparams K;
     unsigned first = 0;
     int rc = prepare(c, p, K, first);
@@ -1576,13 +1684,16 @@ int rt_render_device(rt_context* c, const rt_render_params* p, void* rgba_device
 
 int rt_synchronize(rt_context* c) {
     if (!c) return RT_ERR_INVALID_ARGUMENT;
+    if (c->cpu) return RT_OK;  // CPU renders are synchronous
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->last_stream && c->last_stream != c->stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+    if (c->render_recorded) HIP_TRY(c, hipEventSynchronize(c->ev_render));
+    if (c->aux_recorded) HIP_TRY(c, hipEventSynchronize(c->ev_aux));
     return RT_OK;
 }
 
 float rt_last_kernel_ms(rt_context* c) {
+    if (c && c->cpu) return c->cpu_ms;
     if (!c || !c->timed) return -1.0f;
     if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.0f;
     float ms = -1.0f;
@@ -1595,21 +1706,32 @@ int rt_deinterleave_rows_device(rt_context* c, const void* gathered, void* image
     if (!c || !gathered || !image) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
     if (width <= 0 || height <= 0 || shards <= 0 || rows_per_shard * shards < height)
         return fail(c, RT_ERR_INVALID_ARGUMENT, "bad deinterleave geometry");
+    if (c->cpu) return fail(c, RT_ERR_UNSUPPORTED, "rt_deinterleave_rows_device: CPU context");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIP_TRY(c, rt_launch_deinterleave((const unsigned*)gathered, (unsigned*)image, width, height, shards,
                                       rows_per_shard, s));
-    c->last_stream = s;
+    HIP_TRY(c, hipEventRecord(c->ev_aux, s));
+    c->aux_recorded = true;
     return RT_OK;
 }
 
 int rt_get_state(rt_context* c, uint32_t* rng, float* accum) {
     if (!c) return RT_ERR_INVALID_ARGUMENT;
+    const size_t npix = (size_t)c->rows * c->width;
+    if (c->cpu) {
+        if (c->rng_h.empty()) return fail(c, RT_ERR_INVALID_ARGUMENT, "no shard state (render or rt_init_rand first)");
+        if (rng) std::memcpy(rng, c->rng_h.data(), npix * 6 * sizeof(unsigned));
+        if (accum)
+            for (size_t i = 0; i < npix; i++)
+                for (int ch = 0; ch < 3; ch++) accum[3 * i + ch] = c->accum_h[ch * npix + i];
+        return RT_OK;
+    }
     if (!c->rng.p) return fail(c, RT_ERR_INVALID_ARGUMENT, "no shard state (render or rt_init_rand first)");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->last_stream != c->stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
-    const size_t npix = (size_t)c->rows * c->width;
+    const int qrc = quiesce(c);  // the last render, on whatever stream it ran
+    if (qrc) return qrc;
     if (rng) HIP_TRY(c, hipMemcpy(rng, c->rng.p, npix * 6 * sizeof(unsigned), hipMemcpyDeviceToHost));
     if (accum) {
         std::vector<float> planes(npix * 3);
@@ -1622,12 +1744,20 @@ int rt_get_state(rt_context* c, uint32_t* rng, float* accum) {
 
 int rt_set_state(rt_context* c, const uint32_t* rng, const float* accum, unsigned frame_counter) {
     if (!c) return RT_ERR_INVALID_ARGUMENT;
-    if (!c->rng.p) return fail(c, RT_ERR_INVALID_ARGUMENT, "no shard state (rt_init_rand first)");
+    if (c->cpu ? c->rng_h.empty() : !c->rng.p) return fail(c, RT_ERR_INVALID_ARGUMENT, "no shard state (rt_init_rand first)");
     if (frame_counter == 0) return fail(c, RT_ERR_INVALID_ARGUMENT, "frame_counter must be >= 1");
+    const size_t npix = (size_t)c->rows * c->width;
+    if (c->cpu) {
+        if (rng) std::memcpy(c->rng_h.data(), rng, npix * 6 * sizeof(unsigned));
+        if (accum)
+            for (size_t i = 0; i < npix; i++)
+                for (int ch = 0; ch < 3; ch++) c->accum_h[ch * npix + i] = accum[3 * i + ch];
+        c->frame = frame_counter;
+        return RT_OK;
+    }
     HIP_TRY(c, hipSetDevice(c->device));
     const int rc = quiesce(c);  // a render on a caller's stream may still use the state
     if (rc) return rc;
-    const size_t npix = (size_t)c->rows * c->width;
     std::vector<float> planes;
     if (rng)
         HIP_TRY(c, hipMemcpyAsync(c->rng.p, rng, npix * 6 * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
@@ -1657,5 +1787,14 @@ const char* rt_error_string(int status) {
 }
 
 const char* rt_last_error(const rt_context* c) { return c ? c->err.c_str() : ""; }
+
+int rt_render_cpu(rt_context* c, const rt_render_params* p, int threads, uint8_t* rgba_out, float* accum_out) {
+    if (!c) return RT_ERR_INVALID_ARGUMENT;
+    if (!c->cpu) return fail(c, RT_ERR_INVALID_ARGUMENT, "rt_render_cpu: not a CPU context (rt_create_cpu)");
+    if (threads < 0) return fail(c, RT_ERR_INVALID_ARGUMENT, "threads < 0");
+    return cpu_render(c, p, threads, rgba_out, accum_out);
+}
+
+int rt_context_threads(const rt_context* c) { return c && c->cpu ? c->threads : 0; }
 
 }  // extern "C"

@@ -43,6 +43,7 @@
 #define RT_NEAR_ZERO 0.0001f       // Intersection.cuh:4
 #define RT_SPECULAR_CHANCE 0.5f    // Main.cu:29
 #define RT_PI 3.1415926535f        // Math.cuh:5
+#define RT_MAX_LEVELS 33           // recursion records per path: RT_MAX_BOUNCES (rt_abi.h) + 1
 
 struct rt_kparams {
     int width, height;          // full image
@@ -115,6 +116,11 @@ struct rt_kparams {
     long order_cap;             // capacity of group_order / group_cost
     int leaf_batch;             // BVH refill kernel: leaf tests once this many lanes are ready
     int refill;                 // BVH refill kernel: new rays once this many of 64 (relative) wait
+    // samplesPerPixel (Main.cu:27, 296-299): paths traced per frame from the
+    // frame's one jittered camera ray; the LAST one, scaled by 1/n, is the
+    // frame's sample.  1 (the reference build) everywhere but the simple
+    // kernel and the CPU fallback, which the launch policy picks for n > 1
+    int spp_inner;
 };
 
 // leaf-batch thresholds of the launch policy (full frames / small shards)

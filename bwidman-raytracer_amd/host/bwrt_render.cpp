@@ -8,8 +8,8 @@
 //
 //   bwrt_render [--scene 07|01|04|04_box | --scene-file FILE] [--save-scene FILE]
 //               [--width 1920] [--height 1080] [--frames 8] [--frames-per-call 1]
-//               [--max-bounces 5] [--background r,g,b] [--device 0] [--gpus 1]
-//               [--keys "W*10,W+LEFT*5,*3"] [--dt SECONDS]
+//               [--max-bounces 5] [--background r,g,b] [--spp 1] [--device 0] [--gpus 1]
+//               [--cpu [THREADS]] [--keys "W*10,W+LEFT*5,*3"] [--dt SECONDS]
 //               [--out image.png|image.ppm] [--dump-scene file.bin]
 //
 // --keys: comma-separated steps KEY[+KEY...]*FRAMES (keys W A S D SPACE
@@ -17,6 +17,11 @@
 // the timeline repeats its last step.  ESCAPE ends the loop like
 // glfwSetWindowShouldClose.  --gpus N renders every frame across N contexts
 // (devices device..device+N-1, modulo the visible count) with rt_render_multi.
+// --cpu renders on the library's scalar C++ CPU fallback instead (THREADS
+// host threads, 0 or omitted = all; BASELINE config 1's "scalar C++ CPU
+// path").  --spp sets samplesPerPixel (Main.cu:27; the in-frame loop keeps
+// the last of n paths, Main.cu:296-299), and "Samples:" prints
+// accumulatedFrames * samplesPerPixel like Main.cu:491.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -37,8 +42,8 @@ static int die(rt_context* ctx, int rc, const char* what) {
 static const char* kUsage =
     "usage: bwrt_render [--scene 07|01|04|04_box | --scene-file FILE] [--save-scene FILE]\n"
     "                   [--width 1920] [--height 1080] [--frames 8] [--frames-per-call 1]\n"
-    "                   [--max-bounces 5] [--background r,g,b] [--device 0] [--gpus 1]\n"
-    "                   [--keys \"W*10,W+LEFT*5,*3\"] [--dt SECONDS]\n"
+    "                   [--max-bounces 5] [--background r,g,b] [--spp 1] [--device 0] [--gpus 1]\n"
+    "                   [--cpu [THREADS]] [--keys \"W*10,W+LEFT*5,*3\"] [--dt SECONDS]\n"
     "                   [--out image.png|image.ppm] [--dump-scene file.bin]\n";
 
 struct KeyStep {
@@ -94,7 +99,7 @@ static bool parse_keys(const std::string& spec, std::vector<KeyStep>& steps) {
 int main(int argc, char** argv) {
     std::string scene_name = "07", scene_file, save, out, dump, keys_spec;
     int width = 1920, height = 1080, frames = 8, per_call = 1, max_bounces = RT_DEFAULT_MAX_BOUNCES, device = 0;
-    int gpus = 1;
+    int gpus = 1, spp = 1, cpu_threads = -1;  // -1: GPU
     float bg[3] = {0.0f, 0.0f, 0.0f};
     double fixed_dt = -1.0;
     for (int i = 1; i < argc; i++) {
@@ -117,6 +122,11 @@ int main(int argc, char** argv) {
             }
         } else if (!std::strcmp(argv[i], "--device")) device = std::atoi(next());
         else if (!std::strcmp(argv[i], "--gpus")) gpus = std::atoi(next());
+        else if (!std::strcmp(argv[i], "--spp")) spp = std::atoi(next());
+        else if (!std::strcmp(argv[i], "--cpu")) {
+            cpu_threads = 0;
+            if (i + 1 < argc && argv[i + 1][0] >= '0' && argv[i + 1][0] <= '9') cpu_threads = std::atoi(argv[++i]);
+        }
         else if (!std::strcmp(argv[i], "--keys")) keys_spec = next();
         else if (!std::strcmp(argv[i], "--dt")) fixed_dt = std::atof(next());
         else if (!std::strcmp(argv[i], "--out")) out = next();
@@ -163,13 +173,19 @@ int main(int argc, char** argv) {
     }
     if (!dump.empty() || (!save.empty() && frames <= 0)) return 0;
 
-    if (gpus < 1) gpus = 1;
-    const int ndev = rt_device_count() > 0 ? rt_device_count() : 1;
+    if (gpus < 1 || cpu_threads >= 0) gpus = 1;
+    const int ndev = cpu_threads >= 0 ? 1 : rt_device_count() > 0 ? rt_device_count() : 1;
     std::vector<rt_context*> ctxs(gpus, nullptr);
     int rc = 0;
     rt_scene view = sd.view();
     for (int g = 0; g < gpus; g++) {
-        if ((rc = rt_create((device + g) % ndev, &ctxs[g]))) return die(ctxs[g], rc, "rt_create");
+        if (cpu_threads >= 0) {
+            if ((rc = rt_create_cpu(cpu_threads, &ctxs[g]))) return die(ctxs[g], rc, "rt_create_cpu");
+            std::printf("CPU fallback: %d threads\n", rt_context_threads(ctxs[g]));
+        } else if ((rc = rt_create((device + g) % ndev, &ctxs[g]))) {
+            return die(ctxs[g], rc, "rt_create");
+        }
+        if ((rc = rt_set_samples_per_pixel(ctxs[g], spp))) return die(ctxs[g], rc, "rt_set_samples_per_pixel");
         if ((rc = rt_set_scene(ctxs[g], &view))) return die(ctxs[g], rc, "rt_set_scene");
         if ((rc = rt_set_max_bounces(ctxs[g], max_bounces))) return die(ctxs[g], rc, "rt_set_max_bounces");
         if ((rc = rt_set_background(ctxs[g], bg[0], bg[1], bg[2]))) return die(ctxs[g], rc, "rt_set_background");
@@ -204,7 +220,7 @@ int main(int argc, char** argv) {
         frame_count += n;
         if (delta > 1.0 || done == frames || quit) {  // Main.cu:486-495
             std::printf("FPS: %d | Samples: %u | kernel %.3f ms\n", (int)(frame_count / delta),
-                        rt_frame_counter(ctx) - 1, rt_last_kernel_ms(ctx));
+                        (rt_frame_counter(ctx) - 1) * (unsigned)spp, rt_last_kernel_ms(ctx));
             delta = 0.0;
             frame_count = 0;
         }

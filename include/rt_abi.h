@@ -160,9 +160,39 @@ RT_API rt_material rt_material_default(void);
 /* Number of visible HIP devices (0 when none; never fails). */
 RT_API int rt_device_count(void);
 
-/* Create a context on HIP device `device`. */
+/* Create a context on HIP device `device`.  Without a HIP device this
+ * returns RT_ERR_NO_DEVICE: a GPU context never falls back to the CPU. */
 RT_API int rt_create(int device, rt_context** out);
 RT_API void rt_destroy(rt_context* ctx);
+
+/* ---- scalar C++ CPU fallback ------------------------------------------------
+ * The same per-ray arithmetic as the HIP kernels (csrc/rt_path.h, compiled
+ * for the host), bit-identical results, one pixel per loop iteration on a
+ * pool of `threads` host threads (256-pixel chunks).  It is an explicit
+ * backend, never chosen implicitly: only a context made by rt_create_cpu()
+ * renders on the CPU, and every entry point above behaves on it as on a GPU
+ * context (rt_set_scene, rt_init_rand, rt_render, rt_render_ex, rt_controls,
+ * rt_get_state / rt_set_state, ...; rt_last_kernel_ms gives the last render's
+ * wall time) except rt_render_device, rt_render_multi and
+ * rt_deinterleave_rows_device (RT_ERR_UNSUPPORTED: no device memory).
+ * Replaces the reference's config-1 CPU path and is the CPU baseline of
+ * bench.py (SURVEY §8(b) rt_render_cpu, §8(d)). */
+
+/* Host threads the process may run on (its sched affinity). */
+RT_API int rt_cpu_threads(void);
+
+/* Create a CPU context rendering on `threads` host threads (0 = all of
+ * rt_cpu_threads()).  Needs an x86-64-v3 host (AVX2 + FMA), else
+ * RT_ERR_UNSUPPORTED. */
+RT_API int rt_create_cpu(int threads, rt_context** out);
+
+/* Host threads of a CPU context (0 for a GPU context). */
+RT_API int rt_context_threads(const rt_context* ctx);
+
+/* rt_render_ex() on a CPU context with an explicit thread count for this call
+ * (0 = the context's).  RT_ERR_INVALID_ARGUMENT on a GPU context. */
+RT_API int rt_render_cpu(rt_context* ctx, const rt_render_params* p, int threads,
+                         uint8_t* rgba_out, float* accum_out);
 
 /* Upload a copy of the scene (≈ allocateScene, Main.cu:38-109).  Resets the
  * frame counter to 1, like any camera change in controls().  Waits for a
@@ -187,6 +217,16 @@ RT_API int rt_set_max_bounces(rt_context* ctx, int max_bounces);
  * radiance of a miss and of the depth cut-off (Main.cu:209-211).  Takes
  * effect at the next render; does not reset accumulation. */
 RT_API int rt_set_background(rt_context* ctx, float r, float g, float b);
+
+/* samplesPerPixel (Main.cu:27, a compile-time constant 1 there): each
+ * progressive frame traces n paths from the frame's one jittered camera ray
+ * and, like the reference's loop (Main.cu:296-299, `pixel = tracePath(...)`
+ * assigns), keeps the LAST one, scaled by 1/n; the RNG draws of all n are
+ * consumed.  Default 1, the reference build (and the only value whose frames
+ * are unbiased).  n > 1 renders with the one-path-per-lane kernel.  Takes
+ * effect at the next render; does not reset accumulation. */
+#define RT_MAX_SAMPLES_PER_PIXEL 1024
+RT_API int rt_set_samples_per_pixel(rt_context* ctx, int n);
 
 /* Copy of the context's current camera (after rt_controls()). */
 RT_API int rt_get_camera(const rt_context* ctx, rt_camera* camera);
@@ -250,8 +290,9 @@ RT_API int rt_render_ex(rt_context* ctx, const rt_render_params* p,
 RT_API int rt_render_device(rt_context* ctx, const rt_render_params* p,
                             void* rgba_device, void* stream);
 
-/* Wait for all work of the context (its stream and the last stream passed
- * to rt_render_device). */
+/* Wait for all work of the context: its stream, the last render launch
+ * (also on a caller's stream, rt_render_device) and the last
+ * rt_deinterleave_rows_device. */
 RT_API int rt_synchronize(rt_context* ctx);
 
 /* One image across n contexts in ONE process (one context per GPU, the same

@@ -10,7 +10,26 @@
  *
  * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp; never
  * -ffast-math: the reference's isnan() test must survive, Main.cu:139).
+ *
+ * Pin-sensitivity mutants (test infrastructure for
+ * tests/golden/make_pin_sensitivity.py): -DORC_MUTANT=k replaces ONE
+ * reference quirk by the "natural" formula, to measure
+ * whether the only real-CUDA evidence (Renders/07 and 01 PNGs) can tell them
+ * apart.  The default build has ORC_MUTANT 0: the reference semantics.
+ *   1 A.5  jitter scale 0.001 * (W / 1000.0) instead of integer W / 1000
+ *   2 A.6  half-pixel offset in pixelPosition
+ *   3 A.9  unit triangle / quad shading normals
+ *   4 A.10 tangent-frame helper test not inverted (no zero tangents on n ~ y)
+ *   5 A.11 G1 with tan^2 instead of tan^4
+ *   6 A.11 no isnan(G) guard
+ *   7 A.12 forward-throughput evaluation of the rendering equation
+ *   8 A.14/15 std::min / std::max semantics (NaN propagates) at the clamps
+ *   9      libm sinf / cosf / atanf instead of the Cephes sequence
+ *  (10     FMA contraction: the same source built with -ffp-contract=fast)
  */
+#ifndef ORC_MUTANT
+#define ORC_MUTANT 0
+#endif
 #include "oracle.h"
 
 #include <math.h>
@@ -291,6 +310,9 @@ static int polygon_hit(const ray3* r, const vec3* v, int nv, const orc_material*
         if (dot(inner, sub(info.intersection, v[k])) < 0.0f) return 0;
     }
     *closest = info;
+#if ORC_MUTANT == 3
+    closest->normal = normalize3(closest->normal);
+#endif
     return 1;
 }
 
@@ -298,9 +320,18 @@ static int polygon_hit(const ray3* r, const vec3* v, int nv, const orc_material*
 /* Main.cu:111-206 BRDF helpers */
 static float shadowing_masking(vec3 dir, vec3 n, vec3 m, float rough) { /* :112-120 */
     float vdn = dot(dir, n);
+#if ORC_MUTANT == 8
+    float tt = 1.0f / (vdn * vdn) - 1.0f;
+    float tan_theta = (tt < 0.0f) ? 0.0f : tt;  /* std::max(tt, 0): NaN stays NaN */
+#else
     float tan_theta = fmaxf(1.0f / (vdn * vdn) - 1.0f, 0.0f);
+#endif
+#if ORC_MUTANT == 5
+    return chi(dot(dir, m) / vdn) * 2.0f / (1.0f + sqrtf(1.0f + rough * rough * tan_theta));
+#else
     return chi(dot(dir, m) / vdn) * 2.0f /
            (1.0f + sqrtf(1.0f + rough * rough * tan_theta * tan_theta));
+#endif
 }
 
 static float fresnel(vec3 incident, vec3 normal, float n1, float n2) { /* :122-133 */
@@ -314,7 +345,9 @@ static float fresnel(vec3 incident, vec3 normal, float n1, float n2) { /* :122-1
 
 static float specular_weight(vec3 i, vec3 o, vec3 n, vec3 m, float rough) { /* :135-147 */
     float g = shadowing_masking(i, n, m, rough) * shadowing_masking(o, n, m, rough);
+#if ORC_MUTANT != 6
     if (isnan(g)) return 1.0f;
+#endif
     float den = fabsf(dot(i, n) * dot(m, n));
     if (den == 0.0f) den = NEAR_ZERO;
     return fabsf(dot(i, m)) * g / den;
@@ -322,7 +355,11 @@ static float specular_weight(vec3 i, vec3 o, vec3 n, vec3 m, float rough) { /* :
 
 static vec3 base_around_normal(vec3 m, vec3 n) {                      /* :149-168 */
     vec3 some = v3(1, 0, 0);
+#if ORC_MUTANT == 4
+    if (!(fabsf(dot(n, some)) < 1.0f - NEAR_ZERO)) some = v3(0, 1, 0);
+#else
     if (fabsf(dot(n, some)) < 1.0f - NEAR_ZERO) some = v3(0, 1, 0);
+#endif
     vec3 t1 = cross(n, some);
     vec3 t2 = cross(n, t1);
     mat3 b = {{{t1.x, t2.x, n.x}, {t1.y, t2.y, n.y}, {t1.z, t2.z, n.z}}};
@@ -332,12 +369,22 @@ static vec3 base_around_normal(vec3 m, vec3 n) {                      /* :149-16
 static vec3 microfacet_normal(float rough, uint32_t st[6]) {          /* :170-185 */
     float e1 = rand_range(st, 1.0f);
     float e2 = rand_range(st, 1.0f);
+#if ORC_MUTANT == 9
+#define orc_atanf atanf
+#define orc_sinf sinf
+#define orc_cosf cosf
+#endif
     float theta = orc_atanf(rough * sqrtf(e1) / sqrtf(1.0f - e1));
     float phi = 2.0f * ORC_PI * e2;
     float st_ = orc_sinf(theta);
     float x = st_ * orc_cosf(phi);
     float y = st_ * orc_sinf(phi);
     float z = orc_cosf(theta);
+#if ORC_MUTANT == 9
+#undef orc_atanf
+#undef orc_sinf
+#undef orc_cosf
+#endif
     return v3(x, y, z);
 }
 
@@ -363,6 +410,10 @@ static unsigned long long g_queries, g_paths;
 static vec3 g_background = {0.0f, 0.0f, 0.0f};                        /* Main.cu:27 */
 
 void orc_set_background(float r, float g, float b) { g_background = v3(r, g, b); }
+
+/* samplesPerPixel (Main.cu:27, 1 in the reference build) */
+static int g_spp = 1;
+void orc_set_samples_per_pixel(int n) { g_spp = n > 0 ? n : 1; }
 
 static vec3 trace_path(ray3 in, const orc_scene* sc, uint32_t st[6], int bounces,
                        int max_bounces, unsigned long long* queries) { /* Main.cu:208-272 */
@@ -407,12 +458,62 @@ static vec3 trace_path(ray3 in, const orc_scene* sc, uint32_t st[6], int bounces
     return out;
 }
 
+#if ORC_MUTANT == 7
+/* mutant A.12: the same path, rendering equation evaluated forward
+ * (acc += T * emitted, T *= brdf * cos) instead of innermost-first */
+static vec3 trace_path_forward(ray3 in, const orc_scene* sc, uint32_t st[6], int max_bounces,
+                               unsigned long long* queries) {
+    vec3 acc = v3(0, 0, 0), T = v3(1, 1, 1);
+    for (int bounces = 0;; bounces++) {
+        if (bounces > max_bounces) return add(acc, mulv(T, g_background));
+        (*queries)++;
+        hit_info closest = hit_init();
+        int n = sc->sphere_count;
+        if (sc->plane_count > n) n = sc->plane_count;
+        if (sc->triangle_count > n) n = sc->triangle_count;
+        if (sc->quad_count > n) n = sc->quad_count;
+        int hit = 0;
+        for (int i = 0; i < n; i++) {
+            if (i < sc->sphere_count) hit |= sphere_hit(&in, &sc->spheres[i], &closest);
+            if (i < sc->plane_count) hit |= plane_hit(&in, &sc->planes[i], &closest);
+            if (i < sc->triangle_count)
+                hit |= polygon_hit(&in, sc->triangles[i].vertices, 3, &sc->triangles[i].mat, &closest);
+            if (i < sc->quad_count)
+                hit |= polygon_hit(&in, sc->quads[i].vertices, 4, &sc->quads[i].mat, &closest);
+        }
+        if (!hit) return add(acc, mulv(T, g_background));
+        acc = add(acc, mulv(T, scale(closest.mat.emittance, closest.mat.albedo)));
+        vec3 scatter, brdf;
+        if (rand_range(st, 1.0f) < SPECULAR_CHANCE) {
+            vec3 m = microfacet_normal(closest.mat.roughness, st);
+            m = base_around_normal(m, closest.normal);
+            scatter = reflect3(in.direction, m);
+            float f = fresnel(neg3(in.direction), m, 1.0f, closest.mat.refractive_index);
+            float s = specular_weight(neg3(in.direction), scatter, closest.normal, m, closest.mat.roughness);
+            brdf = scale(s * f / SPECULAR_CHANCE, v3(1, 1, 1));
+        } else {
+            scatter = random_direction(st, closest.normal);
+            brdf = scale((float)(2.0 / (1 - SPECULAR_CHANCE)), closest.mat.albedo);
+        }
+        T = mulv(T, scale(dot(scatter, closest.normal), brdf));
+        in.origin = closest.intersection;
+        in.direction = scatter;
+    }
+}
+#define trace_path(in, sc, st, b, mb, q) trace_path_forward(in, sc, st, mb, q)
+#endif
+
 /* Math.cuh:245-262 */
 static vec3 aces(vec3 c) {
     c = scale(0.6f, c);
     const float a = 2.51f, b = 0.03f, cc = 2.43f, d = 0.59f, e = 0.14f;
     vec3 r = divv(mulv(c, addk(scale(a, c), b)), addk(mulv(c, addk(scale(cc, c), d)), e));
+#if ORC_MUTANT == 8
+#define STD_MIN1(x) ((1.0f < (x)) ? 1.0f : (x)) /* std::min(x, 1): NaN stays NaN */
+    return v3(STD_MIN1(r.x), STD_MIN1(r.y), STD_MIN1(r.z));
+#else
     return v3(fminf(r.x, 1.0f), fminf(r.y, 1.0f), fminf(r.z, 1.0f));
+#endif
 }
 
 static uint8_t to_u8(float v) {                                       /* Main.cu:312 */
@@ -436,7 +537,11 @@ int orc_render_rows(const orc_scene* sc, int width, int height, int row_offset,
     mat3 ru = rot_x(sc->camera.angle[1]);
     mat3 rot = matmul(&rl, &ru);
     /* Main.cu:291: 0.001 * (windowWidth / 1000), double then float */
+#if ORC_MUTANT == 1
+    const float jitter = (float)(0.001 * (width / 1000.0));
+#else
     const float jitter = (float)(0.001 * (width / 1000));
+#endif
     const size_t plane = (size_t)rows * (size_t)width;
     unsigned long long q_total = 0, p_total = 0;
 #ifdef _OPENMP
@@ -457,15 +562,20 @@ int orc_render_rows(const orc_scene* sc, int width, int height, int row_offset,
             vec3 sum = v3(accum[3 * p], accum[3 * p + 1], accum[3 * p + 2]);
             unsigned frame = first_frame;
             for (int f = 0; f < passes; f++, frame++) {
+#if ORC_MUTANT == 2
+                vec3 pix = v3((float)(x - width / 2) + 0.5f, (float)(y - height / 2) + 0.5f, screen_z);
+#else
                 vec3 pix = v3((float)(x - width / 2), (float)(y - height / 2), screen_z);
+#endif
                 pix = matvec(&rot, pix);                              /* :288 */
                 ray3 cam = {sc->camera.position, normalize3(pix)};
                 cam.direction = add(cam.direction,
                                     scale(jitter, random_direction(st, cam.direction)));
                 cam.direction = normalize3(cam.direction);            /* :292 */
                 vec3 val = v3(0, 0, 0);
-                val = trace_path(cam, sc, st, 0, max_bounces, &q);   /* :296-298 */
-                val = scale(1.0f / 1.0f, val);                        /* :299, spp = 1 */
+                for (int i = 0; i < g_spp; i++)                       /* :296-298: assigns */
+                    val = trace_path(cam, sc, st, 0, max_bounces, &q);
+                val = scale(1.0f / (float)g_spp, val);                /* :299, operator/= */
                 if (frame == 1) sum = v3(0, 0, 0);                    /* :301-302 */
                 sum = add(sum, val);                                  /* :304 */
                 p_total++;

@@ -71,6 +71,12 @@ int orc_render_rows(const orc_scene* scene, int width, int height,
  * next orc_render_rows calls. */
 void orc_set_background(float r, float g, float b);
 
+/* samplesPerPixel (Main.cu:27; 1 in the reference build): the in-frame loop
+ * of Main.cu:296-299 traces that many paths from the frame's one jittered
+ * camera ray, keeps the LAST (assignment, not a sum) and scales it by
+ * 1/samplesPerPixel.  Used by the next orc_render_rows calls. */
+void orc_set_samples_per_pixel(int n);
+
 /* Work counters of the last orc_render_rows call (closest-hit queries and
  * paths), for the measured work profile in DESIGN.md. */
 void orc_last_counters(unsigned long long* queries, unsigned long long* paths);

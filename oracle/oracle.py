@@ -30,9 +30,9 @@ def build(force: bool = False) -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        if LIB_PATH_IN_USE == LIB_PATH and not os.path.exists(LIB_PATH):
             build()
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(LIB_PATH_IN_USE)
         L.orc_curand_init.argtypes = [C.c_ulonglong, C.POINTER(C.c_uint32)]
         L.orc_curand_init.restype = None
         L.orc_curand.argtypes = [C.POINTER(C.c_uint32)]
@@ -46,10 +46,24 @@ def lib():
         L.orc_render_rows.restype = C.c_int
         L.orc_set_background.argtypes = [C.c_float, C.c_float, C.c_float]
         L.orc_set_background.restype = None
+        L.orc_set_samples_per_pixel.argtypes = [C.c_int]
+        L.orc_set_samples_per_pixel.restype = None
         L.orc_last_counters.argtypes = [C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
         L.orc_last_counters.restype = None
         _lib = L
     return _lib
+
+
+def use_library(path: str):
+    """Switch to another build of the oracle (the pin-sensitivity mutants,
+    tests/golden/make_pin_sensitivity.py); use_library(LIB_PATH) goes back."""
+    global _lib, LIB_PATH_IN_USE
+    _lib = None
+    LIB_PATH_IN_USE = path
+    return lib()
+
+
+LIB_PATH_IN_USE = LIB_PATH
 
 
 def curand_stream(seed: int, n: int) -> np.ndarray:
@@ -79,10 +93,13 @@ class OracleState:
 
 
 def render(scene, state: OracleState, passes: int, max_bounces: int,
-           first_frame: int | None = None, threads: int = 0, background=(0.0, 0.0, 0.0)) -> np.ndarray:
-    """Render `passes` progressive frames; returns the RGBA8 rows (row 0 = bottom)."""
+           first_frame: int | None = None, threads: int = 0, background=(0.0, 0.0, 0.0),
+           samples_per_pixel: int = 1) -> np.ndarray:
+    """Render `passes` progressive frames; returns the RGBA8 rows (row 0 = bottom).
+    samples_per_pixel: the reference's in-frame loop (Main.cu:27, 296-299)."""
     ff = state.frame if first_frame is None else first_frame
     lib().orc_set_background(*[float(c) for c in background])
+    lib().orc_set_samples_per_pixel(int(samples_per_pixel))
     rc = lib().orc_render_rows(C.cast(scene.ptr(), C.c_void_p), state.width, state.height,
                                state.row_offset, state.row_stride, state.rows, ff, passes,
                                max_bounces, state.rng.ctypes.data, state.accum.ctypes.data,

@@ -51,7 +51,8 @@ def test_error_strings_and_arg_checks(bwrt_lib):
 
 
 def test_no_device_fails_loudly_on_cpu(bwrt_lib):
-    """Without a GPU the product refuses to run (there is no CPU fallback)."""
+    """Without a GPU a GPU context refuses to exist (the CPU fallback is a
+    separate, explicit backend: rt_create_cpu, tests/test_cpu_fallback.py)."""
     if bwrt_lib.rt_device_count() > 0:
         pytest.skip("a GPU is visible")
     ctx = C.c_void_p()

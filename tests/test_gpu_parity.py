@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from bwrt import scenes
+from scenegen import _random_scene, _scaled
 
 pytestmark = pytest.mark.gpu
 
@@ -95,6 +96,82 @@ def test_stress_c5_rows_bvh(gpu, oracle, monkeypatch, n16, mask):
     gpu.set_scene(scenes.scene_07())
     assert np.array_equal(img, st.rgba)
     same_state(gpu, st)
+
+
+def _c5_digests(rgba, acc, rng):
+    import hashlib
+    return {"rgba": hashlib.sha256(np.ascontiguousarray(rgba).tobytes()).hexdigest(),
+            "accum": hashlib.sha256(np.ascontiguousarray(acc).tobytes()).hexdigest(),
+            "rng": hashlib.sha256(np.ascontiguousarray(rng).tobytes()).hexdigest()}
+
+
+def _c5_golden(name):
+    g = json.load(open(os.path.join(GOLDEN, "c5_rows_32spp.json")))
+    return g, g["samples"][name]
+
+
+def test_config5_rows_32spp(gpu):
+    """Config 5 at its own frame count: 8 full-width rows of the stress scene
+    (y = 3 mod 135), 32 spp, 8 bounces, through the default ray-refill
+    kernel, whose lanes refill across frame boundaries — RGBA, frameSum and
+    RNG state bit-exact with the oracle's brute-force loop (its digests,
+    tests/golden/make_c5_golden.py: minutes of oracle time)."""
+    g, smp = _c5_golden("rows8")
+    W, H, spp, mb = g["width"], g["height"], g["spp"], g["max_bounces"]
+    gpu.set_scene(scenes.stress_scene())
+    gpu.init_rand(W, H, smp["row_offset"], smp["row_stride"])
+    img, acc = gpu.render(W, H, spp, mb, first_frame=1, row_offset=smp["row_offset"], row_stride=smp["row_stride"],
+                          want_accum=True)
+    rng, _ = gpu.get_state(smp["rows"], W)
+    gpu.set_scene(scenes.scene_07())
+    got = _c5_digests(img, acc, rng)
+    assert got == {k: smp[k] for k in got}, (got, float(img[0, :, :3].mean()), smp["rgba_first_row_mean"])
+
+
+def test_config5_shard_of_8_32spp(gpu, bwrt_lib):
+    """One of config 5's 8 interleaved-row shards (rows 5, 13, 21, ...: the
+    8-GPU run's per-rank work, rendered under the small-shard launch policy),
+    32 spp, 8 bounces: every 9th row of the GPU shard against the oracle's
+    digests, and the whole shard against the product's CPU fallback (itself
+    pinned to the same digests, tests/test_cpu_fallback.py)."""
+    from bwrt import Renderer
+    g, smp = _c5_golden("rows15")
+    W, H, spp, mb = g["width"], g["height"], g["spp"], g["max_bounces"]
+    s = scenes.stress_scene()
+    gpu.set_scene(s)
+    gpu.init_rand(W, H, 5, 8)
+    img, acc = gpu.render(W, H, spp, mb, first_frame=1, row_offset=5, row_stride=8, want_accum=True)
+    rng, _ = gpu.get_state(135, W)
+    gpu.set_scene(scenes.scene_07())
+    got = _c5_digests(img[::9], acc[::9], rng[:, ::9])
+    assert got == {k: smp[k] for k in got}, got
+    with Renderer.cpu(0, lib=bwrt_lib) as c:
+        c.set_scene(s)
+        c.init_rand(W, H, 5, 8)
+        cimg, cacc = c.render(W, H, spp, mb, first_frame=1, row_offset=5, row_stride=8, want_accum=True)
+        crng, _ = c.get_state(135, W)
+    assert np.array_equal(cimg, img)
+    assert np.array_equal(crng, rng)
+    assert np.array_equal(cacc, acc, equal_nan=True)
+
+
+def test_cpu_fallback_equals_gpu_config3(gpu, bwrt_lib):
+    """The product's scalar C++ CPU fallback (rt_render_cpu, all host cores)
+    and the HIP kernel on BASELINE config 3 in full: the same bits."""
+    from bwrt import Renderer
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    gpu.init_rand(1920, 1080)
+    img, acc = gpu.render(1920, 1080, 8, 4, first_frame=1, want_accum=True)
+    with Renderer.cpu(0, lib=bwrt_lib) as c:
+        c.set_scene(s)
+        c.init_rand(1920, 1080)
+        cimg, cacc = c.render(1920, 1080, 8, 4, first_frame=1, want_accum=True)
+        crng, _ = c.get_state(1080, 1920)
+    rng, _ = gpu.get_state(1080, 1920)
+    assert np.array_equal(cimg, img)
+    assert np.array_equal(cacc, acc, equal_nan=True)
+    assert np.array_equal(crng, rng)
 
 
 @pytest.mark.parametrize("batch,refill", [(1, 1), (64, 64), (33, 1), (1, 64), (60, 36)])
@@ -310,6 +387,28 @@ def test_background_color(gpu, oracle):
     assert img[-1, 0, 2] > 100  # the sky (top row) is now blue
 
 
+@pytest.mark.parametrize("spp,mb", [(3, 4), (2, 8)])
+def test_samples_per_pixel_in_frame_loop(gpu, oracle, spp, mb):
+    """samplesPerPixel > 1 (Main.cu:27, 296-299; the launch policy takes the
+    one-path-per-lane kernel): n paths from one jittered camera ray per
+    frame, the last one kept and scaled by 1/n — bit-exact with the oracle."""
+    s = scenes.scene_07() if mb == 4 else scenes.stress_scene()
+    gpu.set_scene(s)
+    gpu.set_samples_per_pixel(spp)
+    try:
+        gpu.init_rand(96, 54)
+        gpu.render(96, 54, 2, mb, first_frame=1)
+        img = gpu.render(96, 54, 1, mb)
+    finally:
+        gpu.set_samples_per_pixel(1)
+        gpu.set_scene(scenes.scene_07())
+    st = oracle.OracleState(96, 54)
+    oracle.render(s, st, 2, mb, first_frame=1, samples_per_pixel=spp)
+    oracle.render(s, st, 1, mb, samples_per_pixel=spp)
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
 def test_converges_to_reference_png(gpu):
     """Real-CUDA sanity (statistical): 1024 frames of the 07 scene at
     1920x1080, maxBounces 5 (Main.cu:26) vs Renders/07_specular_BRDF.png:
@@ -414,6 +513,28 @@ def test_state_writes_wait_for_device_render(gpu, oracle):
         gpu.set_state(seeds.rng, np.zeros((h, w, 3), np.float32), 1)
         rng, _ = gpu.get_state(h, w)
         assert np.array_equal(rng, seeds.rng)
+    # a de-interleave on a second, unordered stream between the render and the
+    # state writes: the writes wait for the render itself (its event), not for
+    # the last stream used, and that stream may be gone by the next write
+    g = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    out = torch.empty_like(g)
+    for _ in range(2):
+        gpu.set_scene(s07)
+        gpu.init_rand(w, h)
+        gpu.render_device(gpu.params(w, h, spp, mb, first_frame=1), buf.data_ptr(), stream.cuda_stream)
+        s2 = torch.cuda.Stream()
+        gpu.deinterleave_device(g.data_ptr(), out.data_ptr(), w, h, 1, h, s2.cuda_stream)
+        gpu.set_scene(s04)
+        stream.synchronize()
+        assert np.array_equal(buf.cpu().numpy().view(np.uint8).reshape(h, w, 4), st.rgba)
+        s2.synchronize()
+        del s2
+        gpu.set_scene(s07)
+        gpu.render_device(gpu.params(w, h, spp, mb, first_frame=1), buf.data_ptr(), stream.cuda_stream)
+        gpu.init_rand(w, h)
+        rng, _ = gpu.get_state(h, w)
+        assert np.array_equal(rng, seeds.rng)
+        gpu.synchronize()
     # device render on a torch stream, then a synchronous continuation on
     # the context's stream: frames 1..4 then 5..8 equal one 8-frame render
     gpu.init_rand(w, h)
@@ -501,67 +622,6 @@ def test_render_multi_contexts(bwrt_lib, oracle, n):
     finally:
         for r in rs:
             r.close()
-
-
-def _random_scene(seed):
-    """Seeded random scene with the awkward cases the reference's arithmetic
-    meets: rays starting inside spheres (camera inside one), shared triangle
-    edges (ties), degenerate (zero-area) triangles, non-planar / non-convex
-    quads, planes with non-unit normals, roughness 0 and 1, IOR 1 (no
-    Fresnel contrast), emitters of every primitive kind."""
-    import ctypes as C
-    from bwrt.abi import Camera, Plane, Quad, Sphere, Triangle, Vec3
-    rng = np.random.default_rng(seed)
-    U = lambda a, b, n=None: rng.uniform(a, b, n)  # noqa: E731
-    v = lambda p: Vec3(*map(float, p))  # noqa: E731
-
-    def mat():
-        m = scenes.material(tuple(U(0, 1, 3)), float(rng.choice([0, 0, 0, U(1, 20)])),
-                            float(rng.choice([0.0, 1.0, U(0, 1), U(0, 0.05)])),
-                            float(rng.choice([1.0, 1.05, U(1, 10)])))
-        return m
-    cam = Camera(v(U(-1, 1, 3) + [0, 1, 0]), (C.c_float * 2)(*map(float, U(-0.6, 0.6, 2))),
-                 float(U(0.8, 2.2)))
-    sph = [Sphere(v(U(-4, 4, 3) + [0, 1, -6]), float(U(0.2, 2)), mat()) for _ in range(int(rng.integers(0, 6)))]
-    if seed % 3 == 0:  # camera inside a sphere
-        sph.append(Sphere(v([cam.position.x, cam.position.y, cam.position.z]), 0.5, mat()))
-    pln = [Plane(v([0, 0, 0]), (Vec3 * 2)(v([0, 0, float(U(0.5, 3))]), v([float(U(0.5, 3)), 0, 0])), mat())]
-    if seed % 2:
-        pln.append(Plane(v([0, 0, -12]), (Vec3 * 2)(v(U(-1, 1, 3)), v(U(-1, 1, 3))), mat()))
-    tri = []
-    for _ in range(int(rng.integers(0, 8))):
-        a, b, c = (U(-3, 3, 3) + [0, 1.5, -5] for _ in range(3))
-        tri.append(Triangle((Vec3 * 3)(v(a), v(b), v(c)), mat()))
-        if rng.random() < 0.5:  # neighbour sharing the edge a-b
-            d = U(-3, 3, 3) + [0, 1.5, -5]
-            tri.append(Triangle((Vec3 * 3)(v(b), v(a), v(d)), mat()))
-    tri.append(Triangle((Vec3 * 3)(v([0, 1, -4]), v([1, 1, -4]), v([2, 1, -4])), mat()))  # zero area
-    quads = []
-    for _ in range(int(rng.integers(0, 4))):
-        pts = [U(-3, 3, 3) + [0, 1.5, -7] for _ in range(4)]
-        quads.append(Quad((Vec3 * 4)(*[v(p) for p in pts]), mat()))
-    return scenes.Scene(cam, sph, pln, tri, quads, name=f"random{seed}")
-
-
-def _scaled(scene, k):
-    """The same scene with every coordinate (camera, primitives) times k."""
-    for arr, n in zip((scene.spheres, scene.planes, scene.triangles, scene.quads), scene.counts):
-        for i in range(n):
-            p = arr[i]
-            for name in ("position", "origin"):
-                if hasattr(p, name):
-                    q = getattr(p, name)
-                    q.x, q.y, q.z = q.x * k, q.y * k, q.z * k
-            if hasattr(p, "radius"):
-                p.radius = p.radius * k
-            for vs in ("vertices",):
-                if hasattr(p, vs):
-                    for q in getattr(p, vs):
-                        q.x, q.y, q.z = q.x * k, q.y * k, q.z * k
-    c = scene.camera
-    c.position.x, c.position.y, c.position.z = c.position.x * k, c.position.y * k, c.position.z * k
-    scene.set_camera(c)
-    return scene
 
 
 @pytest.mark.parametrize("seed", list(range(40)))

@@ -83,4 +83,5 @@ def test_sqrt_rcp_helpers_exhaustive():
     assert os.path.exists(exe), "build/sqrtx missing: run __graft_entry__.build()"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
+    assert "inputs evaluated: 4294967296 of 4294967296" in r.stdout, r.stdout
     assert r.stdout.count(": 0 mismatches") == 3, r.stdout

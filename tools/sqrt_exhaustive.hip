@@ -2,8 +2,10 @@
 // correctly rounded lowering over every fp32 bit pattern (NaN == NaN):
 // sqrt_cr(x) == sqrtf(x), rcp_cr(x) == 1.0f / x,
 // inv_length_cr(x) == 1.0f / sqrtf(x).
-// Build: hipcc -O2 --offload-arch=gfx950 -Ibwidman-raytracer_amd/csrc -o build/sqrtx tools/sqrt_exhaustive.hip
-// Exit status 0 iff there is no mismatch.
+// Build: make -C bwidman-raytracer_amd sqrtx (the library's own HIPCC and
+// HIPFLAGS, so the check runs the code generation that ships) -> build/sqrtx
+// Exit status 0 iff every one of the 2^32 inputs was evaluated (counted on
+// the device) and there is no mismatch; 2 on a HIP error.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -13,8 +15,10 @@ __device__ __forceinline__ bool differ(float a, float b) {
     return __float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b);
 }
 
-__global__ void check(unsigned long long base, unsigned long long* bad, unsigned* first) {
+__global__ void check(unsigned long long base, unsigned long long* bad, unsigned* first,
+                      unsigned long long* evaluated) {
     const unsigned bits = (unsigned)(base + (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x);
+    if ((threadIdx.x & 63) == 0) atomicAdd(evaluated, (unsigned long long)__popcll(__ballot(1)));
     const float x = __uint_as_float(bits);
     const int k = differ(sqrt_cr(x), sqrtf(x)) ? 0 : differ(rcp_cr(x), 1.0f / x) ? 1
                 : differ(inv_length_cr(x), 1.0f / sqrtf(x)) ? 2 : -1;
@@ -24,17 +28,33 @@ __global__ void check(unsigned long long base, unsigned long long* bad, unsigned
     }
 }
 
+#define HIP_OK(x)                                                                  \
+    do {                                                                           \
+        const hipError_t e_ = (x);                                                 \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));               \
+            return 2;                                                              \
+        }                                                                          \
+    } while (0)
+
 int main() {
     unsigned long long* bad;
     unsigned* first;
-    if (hipMalloc(&bad, 24) != hipSuccess || hipMalloc(&first, 96) != hipSuccess) return 2;
-    (void)hipMemset(bad, 0, 24);
+    HIP_OK(hipMalloc(&bad, 32));  // [0..2] mismatches per helper, [3] inputs evaluated
+    HIP_OK(hipMalloc(&first, 96));
+    HIP_OK(hipMemset(bad, 0, 32));
     const unsigned long long total = 1ull << 32, chunk = 1ull << 28;
-    for (unsigned long long b = 0; b < total; b += chunk) check<<<chunk / 256, 256>>>(b, bad, first);
-    unsigned long long h[3] = {};
+    for (unsigned long long b = 0; b < total; b += chunk) {
+        check<<<chunk / 256, 256>>>(b, bad, first, bad + 3);
+        HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipDeviceSynchronize());
+    unsigned long long h[4] = {};
     unsigned f[24] = {};
-    if (hipMemcpy(h, bad, 24, hipMemcpyDeviceToHost) != hipSuccess) return 2;
-    (void)hipMemcpy(f, first, 96, hipMemcpyDeviceToHost);
+    HIP_OK(hipMemcpy(h, bad, 32, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(f, first, 96, hipMemcpyDeviceToHost));
+    printf("inputs evaluated: %llu of %llu\n", h[3], total);
+    if (h[3] != total) return 1;
     const char* nm[3] = {"sqrt_cr vs sqrtf", "rcp_cr vs 1/x", "inv_length_cr vs 1/sqrtf"};
     for (int k = 0; k < 3; k++) {
         printf("%s over 2^32 inputs: %llu mismatches\n", nm[k], h[k]);
