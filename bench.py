@@ -96,8 +96,8 @@ def cpu_baseline(lib, config, scene_key, w, h, spp, mb, threads, gpu_renderer=No
     baseline ("fallback"), never the measured product.  With gpu_renderer the
     sample is also rendered on the GPU from the same seeds and compared."""
     stride = CPU_SAMPLE_ROW_STRIDE.get(config, 1)
-    aff = lib.rt_cpu_threads()
-    threads = threads if threads > 0 else aff
+    aff = len(os.sched_getaffinity(0))
+    threads = threads if threads > 0 else lib.rt_cpu_threads()  # affinity capped by the cgroup quota
     scene = scenes.SCENES[scene_key]()
     with Renderer.cpu(threads, lib=lib) as c:
         c.set_scene(scene)

@@ -875,14 +875,25 @@ int rt_create_cpu(int threads, rt_context** out) {
 }
 
 int rt_cpu_threads(void) {
-    // the CPUs this process may run on (sched affinity), not the machine's
+    // the CPUs this process may run on (sched affinity), not the machine's,
+    // capped by a cgroup v2 CPU quota (cpu.max "quota period", rounded up):
+    // a container may see every CPU of the host but be granted a share
+    int n = 0;
     cpu_set_t set;
-    if (sched_getaffinity(0, sizeof set, &set) == 0) {
-        const int n = CPU_COUNT(&set);
-        if (n > 0) return n;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    if (n <= 0) n = 1;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char quota[32] = {0};
+        long period = 0;
+        if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0) {
+            const long q = std::atol(quota);
+            const int share = (int)((q + period - 1) / period);
+            if (share > 0 && share < n) n = share;
+        }
+        std::fclose(f);
     }
-    const unsigned n = std::thread::hardware_concurrency();
-    return n > 0 ? (int)n : 1;
+    return n;
 }
 
 void rt_destroy(rt_context* c) {

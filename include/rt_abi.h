@@ -178,7 +178,8 @@ RT_API void rt_destroy(rt_context* ctx);
  * Replaces the reference's config-1 CPU path and is the CPU baseline of
  * bench.py (SURVEY §8(b) rt_render_cpu, §8(d)). */
 
-/* Host threads the process may run on (its sched affinity). */
+/* Host threads the process may run on: its sched affinity, capped by a
+ * cgroup v2 CPU quota (/sys/fs/cgroup/cpu.max) when one is set. */
 RT_API int rt_cpu_threads(void);
 
 /* Create a CPU context rendering on `threads` host threads (0 = all of

@@ -18,7 +18,8 @@ __device__ __forceinline__ bool differ(float a, float b) {
 __global__ void check(unsigned long long base, unsigned long long* bad, unsigned* first,
                       unsigned long long* evaluated) {
     const unsigned bits = (unsigned)(base + (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x);
-    if ((threadIdx.x & 63) == 0) atomicAdd(evaluated, (unsigned long long)__popcll(__ballot(1)));
+    const unsigned long long wave = __ballot(1);  // (taken by the whole wave, before the branch)
+    if ((threadIdx.x & 63) == 0) atomicAdd(evaluated, (unsigned long long)__popcll(wave));
     const float x = __uint_as_float(bits);
     const int k = differ(sqrt_cr(x), sqrtf(x)) ? 0 : differ(rcp_cr(x), 1.0f / x) ? 1
                 : differ(inv_length_cr(x), 1.0f / sqrtf(x)) ? 2 : -1;
