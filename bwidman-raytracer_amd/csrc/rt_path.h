@@ -567,13 +567,20 @@ RT_HD int ray_octant(const rt_kparams& K, f3 d) {
 // The ray may enter box [lo, hi] before the closest hit so far: margins of
 // 1e-5 relative + m absolute on the interval, and prune against the current
 // closest distance only beyond the same margins
-RT_HD bool slab_enter(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float best_t) {
+// (slab_test also returns the box's entry / exit distances)
+RT_HD bool slab_test(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float best_t,
+                     float& tmin, float& tmax) {
     const float tx0 = __builtin_fmaf(lx, s.inv.x, -s.oinv.x), tx1 = __builtin_fmaf(hx, s.inv.x, -s.oinv.x);
     const float ty0 = __builtin_fmaf(ly, s.inv.y, -s.oinv.y), ty1 = __builtin_fmaf(hy, s.inv.y, -s.oinv.y);
     const float tz0 = __builtin_fmaf(lz, s.inv.z, -s.oinv.z), tz1 = __builtin_fmaf(hz, s.inv.z, -s.oinv.z);
-    const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
     return tmin <= tmax * (1.0f + 1e-5f) + s.m && tmin <= best_t * (1.0f + 1e-5f) + (1e-5f + s.m);
+}
+
+RT_HD bool slab_enter(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float best_t) {
+    float tmin, tmax;
+    return slab_test(lx, ly, lz, hx, hy, hz, s, best_t, tmin, tmax);
 }
 
 // Leaf record (rt_layout.h RT_LEAF_FLOATS) {key, record...}: kind = key & 3,

@@ -19,6 +19,10 @@ formula, runs both checks on every mutant, and records:
   pixels_differing_vs_oracle / frame_sum_pixels_differing_vs_oracle
                     pixels whose RGBA8 / float frameSum differ from the
                     unmutated oracle's (what the bit-exact tests see)
+  png_where_it_differs  a sharper reading of the same PNG: only the 16x16
+                    block channels where mutant and oracle differ by more
+                    than 2 LSB (beyond the 1024-frame noise), each one's MAE
+                    against the PNG there and how often the mutant is closer
 
 -> tests/golden/pin_sensitivity.json (read by tests/test_oracle.py).
 
@@ -69,13 +73,30 @@ def build(k):
     return out
 
 
-def block_mae(rgba, g):
+def render_blocks(rgba, g):
     top = rgba[::-1, :, :3]
     dx, dy, ph, pw, b = (int(g[k]) for k in ("dx", "dy", "png_h", "png_w", "block"))
     crop = top[dy:dy + ph, dx:dx + pw]
     hh, ww = ph // b * b, pw // b * b
-    blocks = crop[:hh, :ww].astype(np.float64).reshape(hh // b, b, ww // b, b, 3).mean((1, 3))
-    return float(np.abs(blocks - g["blocks"]).mean())
+    return crop[:hh, :ww].astype(np.float64).reshape(hh // b, b, ww // b, b, 3).mean((1, 3))
+
+
+def block_mae(rgba, g):
+    return float(np.abs(render_blocks(rgba, g) - g["blocks"]).mean())
+
+
+def discriminating(mut_blocks, base_blocks, g, thresh=2.0):
+    """The PNG's verdict where the mutant's effect exceeds the noise: block
+    channels whose means differ by more than `thresh` LSB between mutant and
+    oracle, and each one's MAE against the PNG there."""
+    sel = np.abs(mut_blocks - base_blocks) > thresh
+    n = int(sel.sum())
+    if n == 0:
+        return {"block_channels": 0}
+    png = g["blocks"]
+    em, eb = np.abs(mut_blocks - png)[sel], np.abs(base_blocks - png)[sel]
+    return {"block_channels": n, "threshold_lsb": thresh, "mutant_mae": round(float(em.mean()), 4),
+            "oracle_mae": round(float(eb.mean()), 4), "mutant_closer_frac": round(float((em < eb).mean()), 4)}
 
 
 def disc_check(g):
@@ -123,13 +144,17 @@ def main():
             base_acc = np.load(os.path.join(ORACLE, "_mut", "base_acc.npy"))
         acc_diff = ~((st.accum == base_acc) | (np.isnan(st.accum) & np.isnan(base_acc)))
         mae = block_mae(st.rgba, g07)
+        np.save(os.path.join(ORACLE, "_mut", f"rgba_m{k}.npy"), st.rgba)
+        base_rgba = np.load(os.path.join(ORACLE, "_mut", "rgba_m0.npy"))
+        disc_blocks = discriminating(render_blocks(st.rgba, g07), render_blocks(base_rgba, g07), g07)
         name, what = MUTANTS[k]
         res["mutants"][str(k)] = {
             "name": name, "change": what, "mae_vs_png": round(mae, 4), "png_check_passes": mae <= 1.5,
             "disc": disc_check(g01),
             "mean_abs_diff_vs_oracle": round(float(np.abs(rgb - base_rgb).mean()), 4),
             "pixels_differing_vs_oracle": int((rgb != base_rgb).any(-1).sum()),
-            "frame_sum_pixels_differing_vs_oracle": int(acc_diff.any(-1).sum())}
+            "frame_sum_pixels_differing_vs_oracle": int(acc_diff.any(-1).sum()),
+            "png_where_it_differs": disc_blocks}
         print(f"mutant {k} ({name}): MAE {mae:.3f}, disc {res['mutants'][str(k)]['disc']['passes']}, "
               f"|diff| {res['mutants'][str(k)]['mean_abs_diff_vs_oracle']} ({time.time() - t0:.0f} s)", flush=True)
         with open(out_path, "w") as f:
