@@ -878,12 +878,6 @@ rt_render_sorted_kernel(rt_kparams K) {
 // 62 / 64 (all lanes, Aila & Laine's rule): 102.2 / 99.1 / 98.1 / 97.3 / 98.2
 // / 101.1 / 118.0 ms, its 1/8 shard 24.8 / 23.4 / 23.0 / 22.3 / 22.2 / 22.3 /
 // 25.5 ms; with two, 60 / 62: 91.8 / 92.6 ms, 1/8 shard 21.3 / 20.2 ms
-// leaf parking of the node loop: 2 = a lane parks up to two leaves and walks
-// on past the first (speculative, Aila & Laine), stalling at a third; 1 = a
-// lane stops at its first leaf until the batch has tested it (A/B builds)
-#ifndef RT_PARK
-#define RT_PARK 2
-#endif
 // fp16 bits -> float (exact)
 __device__ __forceinline__ float h2f(unsigned bits) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)(bits & 0xffffu));
@@ -913,9 +907,6 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     bool pending = false;    // a finished query waits to be shaded
     bool idle = false;       // no pixel left
     int node = -1, leaf = -1, leaf2 = -1;  // two parked leaves per lane
-#if RT_PARK == 3
-    float spec_lim = INFINITY;  // exit distance of the first parked leaf
-#endif
     float best_t = INFINITY;
     int best_id = -1, best_key = -1;
     SlabRay sr;
@@ -1062,11 +1053,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
         while (true) {
             while (true) {  // node steps; a lane parks the first two leaves its ray enters
                 bool stalled = false;
-#if RT_PARK == 1
-                if (walking && node >= 0 && leaf < 0) {  // non-speculative: no steps past a parked leaf
-#else
                 if (walking && node >= 0) {
-#endif
                     RT_BRANCH_COUNT(K, 5);
                     float4 lo, hi;
                     if (N16) {
@@ -1080,41 +1067,18 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                         lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
                         hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
                     }
-#if RT_PARK == 3
-                    float tmin, tmax;
-                    const bool hit = slab_test(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, sr, best_t, tmin, tmax);
-#else
                     const bool hit = slab_enter(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, sr, best_t);
-#endif
                     const int miss = __float_as_int(lo.w);
                     const int lf = __float_as_int(hi.w);
                     // branch-free step: miss -> skip the subtree; internal -> first
                     // child; leaf -> park it (or stall on a third one)
                     const bool is_leaf = hit && lf >= 0;
-#if RT_PARK == 3
-                    // bounded speculation: with a leaf parked, a node the ray enters
-                    // only beyond that leaf's exit distance waits for the batch (a hit
-                    // in the leaf would prune it; without one the walk resumes there)
-                    const bool beyond = hit && leaf >= 0 && tmin > spec_lim;
-                    stalled = beyond || (is_leaf && leaf2 >= 0);
-                    const bool park = !beyond && is_leaf && leaf2 < 0;
-                    spec_lim = park && leaf < 0 ? tmax : spec_lim;
-                    leaf2 = park && leaf >= 0 ? lf : leaf2;
-                    leaf = park && leaf < 0 ? lf : leaf;
-                    node = beyond ? node : (!hit || park ? miss : (is_leaf ? node : node + 1));
-                }
-#elif RT_PARK == 1
-                    leaf = is_leaf ? lf : leaf;
-                    node = !hit || is_leaf ? miss : node + 1;
-                }
-#else
                     stalled = is_leaf && leaf2 >= 0;
                     const bool park = is_leaf && leaf2 < 0;
                     leaf2 = park && leaf >= 0 ? lf : leaf2;
                     leaf = park && leaf < 0 ? lf : leaf;
                     node = !hit || park ? miss : (is_leaf ? node : node + 1);
                 }
-#endif
                 // test the parked leaves once K.leaf_batch of the 64 lanes are
                 // ready (a leaf parked, the walk done or stalled, no walk);
                 // the rest walk on and join a later batch
@@ -1139,9 +1103,6 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                               best_key);
                 leaf2 = -1;
             }
-#if RT_PARK == 3
-            spec_lim = INFINITY;
-#endif
             STAMP(2);
             if (walking && node < 0) {  // walk complete: the query result is best_t / best_id
                 walking = false;
