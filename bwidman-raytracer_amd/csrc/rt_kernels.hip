@@ -884,8 +884,10 @@ __device__ __forceinline__ float h2f(unsigned bits) {
 }
 
 // N16: 16-byte nodes (rt_layout.h bvh_nodes16) — one gather per node visit
-// instead of two; the walk, its tests and its order are the same
-template <int BLOCK, bool N16>
+// instead of two; the walk, its tests and its order are the same.
+// ORDER: launch-order feedback as in the sorted kernel (workgroup g renders
+// tile-group group_order[g] and records its duration in group_cost[])
+template <int BLOCK, bool N16, bool ORDER = false>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
 rt_render_bvh_refill_kernel(rt_kparams K) {
     extern __shared__ float smem[];
@@ -897,8 +899,10 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     const long npix = (long)K.rows * K.width;
     const long T = (long)gridDim.x * BLOCK;
     const long nitems = items_of(K, npix);
+    const long group = ORDER && K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
+    if (ORDER && tid == 0) K.group_cost[group] = (unsigned)__builtin_amdgcn_s_memrealtime();
     PixelState px;
-    load_item(K, npix, nitems, (long)blockIdx.x * BLOCK + tid, px);
+    load_item(K, npix, nitems, group * BLOCK + tid, px);
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -1115,6 +1119,10 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             if (w == 0ull || 64 * __popcll(__ballot(!walking && !idle)) >= K.refill * __popcll(__ballot(!idle))) break;
         }
     }
+    if (ORDER && tid == 0) {  // the loop exit is wave-uniform (one wave per group)
+        const long g = K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
+        K.group_cost[g] = (unsigned)__builtin_amdgcn_s_memrealtime() - K.group_cost[g];
+    }
 #ifdef RT_STAMPS
     if ((threadIdx.x & 63) == 0 && K.stamps)
         for (int k = 0; k < 6; k++) atomicAdd(&K.stamps[k], st_acc[k]);
@@ -1214,22 +1222,47 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
 // (rt_kernels_bvh.hip), built at -O3: the traversal loops want the full
 // optimizer while the brute-force kernels are faster at -O1.
 // BVH scenes by default: the ray-refill kernel, 64-lane groups (no barriers)
-hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, hipStream_t s) {
+hipError_t rt_launch_render_bvh_refill(const rt_kparams& K0, int num_cus, hipStream_t s) {
     constexpr int BLOCK = 64;
+    rt_kparams K = K0;
     long nitems = (long)K.rows * K.width;
     if (K.tile_w > 0) {
         const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
         nitems = tiles_x * tiles_y * 64;
     }
-    const long grid = (nitems + BLOCK - 1) / BLOCK;
+    const long grid = (nitems + BLOCK - 1) / BLOCK < 1 ? 1 : (nitems + BLOCK - 1) / BLOCK;
     const size_t lds = (size_t)3 * (K.max_bounces + 1) * BLOCK * sizeof(float);
-    if (K.bvh_nodes16)
-        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, true>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(BLOCK),
-                           lds, s, K);
+    // launch-order feedback (as launch_render): only for grids of more than
+    // RT_ORDER_MIN_GEN generations of resident groups
+    bool feedback = K.group_cost && K.group_order && grid <= K.order_cap;
+    if (feedback) {
+        int per_cu = 0;
+        const void* kp = K.bvh_nodes16 ? reinterpret_cast<const void*>(&rt_render_bvh_refill_kernel<BLOCK, true, true>)
+                                       : reinterpret_cast<const void*>(&rt_render_bvh_refill_kernel<BLOCK, false, true>);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, BLOCK, lds) != hipSuccess || per_cu <= 0)
+            per_cu = 1;
+        feedback = (double)grid > RT_ORDER_MIN_GEN * (double)per_cu * num_cus;
+    }
+    if (!feedback) {
+        K.group_cost = nullptr;
+        K.group_order = nullptr;
+    } else if (K.order_n != grid) {
+        K.group_order = nullptr;  // no order for this grid yet: blockIdx order
+    }
+    if (feedback && K.bvh_nodes16)
+        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, true, true>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
+    else if (feedback)
+        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false, true>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
+    else if (K.bvh_nodes16)
+        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, true>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
     else
-        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false>), dim3((unsigned)(grid < 1 ? 1 : grid)),
-                           dim3(BLOCK), lds, s, K);
-    return hipGetLastError();
+        hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && feedback) {
+        e = rt_launch_order_groups(K0.group_cost, K0.group_order, grid, s);
+        if (e == hipSuccess) rt_order_groups_last = grid;
+    }
+    return e;
 }
 
 hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
@@ -1250,7 +1283,7 @@ hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, siz
 #else
 hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
                                 hipStream_t s);
-hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, hipStream_t s);
+hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, int num_cus, hipStream_t s);
 
 namespace {
 template <int BLOCK, bool SORTED>
@@ -1322,7 +1355,7 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     // samplesPerPixel > 1 (the reference's in-frame loop, off by default):
     // only the one-path-per-lane kernel implements it
     simple = simple || K.spp_inner > 1;
-    if (K.bvh_nodes && bvh_refill && !simple && block_req == 0) return rt_launch_render_bvh_refill(K, stream);
+    if (K.bvh_nodes && bvh_refill && !simple && block_req == 0) return rt_launch_render_bvh_refill(K, num_cus, stream);
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = !K.bvh_nodes && (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
     const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 49152;

@@ -720,6 +720,40 @@ def test_bvh_through_sorted_kernel(bwrt_lib, oracle, monkeypatch, name):
         r.close()
 
 
+def test_launch_order_feedback_bvh_refill(bwrt_lib, monkeypatch):
+    """Launch-order feedback in the BVH ray-refill kernel (config 5's
+    product path): the stress scene at 1920x1080, 2 spp, 8 bounces — a grid
+    of 32,400 single-wave groups, several resident generations — rendered
+    four times (blockIdx order, then each launch in the order sorted from the
+    last) and once as a continuation; every image, frameSum and RNG state
+    equals the product's CPU fallback (itself pinned to the oracle,
+    tests/test_cpu_fallback.py; the brute-force oracle would need minutes)."""
+    from bwrt import Renderer
+    s = scenes.stress_scene()
+    with Renderer.cpu(0, lib=bwrt_lib) as c:
+        c.set_scene(s)
+        c.init_rand(1920, 1080)
+        want = c.render(1920, 1080, 2, 8, first_frame=1, want_accum=True)
+        want_rng, _ = c.get_state(1080, 1920)
+        cont = c.render(1920, 1080, 1, 8, want_accum=True)
+        cont_rng, _ = c.get_state(1080, 1920)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
+    try:
+        r.set_scene(s)
+        for _ in range(4):
+            r.init_rand(1920, 1080)
+            img, acc = r.render(1920, 1080, 2, 8, first_frame=1, want_accum=True)
+            rng, _ = r.get_state(1080, 1920)
+            assert np.array_equal(img, want[0]) and np.array_equal(acc, want[1], equal_nan=True)
+            assert np.array_equal(rng, want_rng)
+        img, acc = r.render(1920, 1080, 1, 8, want_accum=True)
+        rng, _ = r.get_state(1080, 1920)
+        assert np.array_equal(img, cont[0]) and np.array_equal(acc, cont[1], equal_nan=True)
+        assert np.array_equal(rng, cont_rng)
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("scene_name,w,h,spp,mb,grec", [("07", 1920, 1080, 2, 4, 0), ("04", 1600, 1200, 2, 3, 0),
                                                        ("07", 1920, 1080, 2, 6, 1)])
 def test_launch_order_feedback(bwrt_lib, oracle, monkeypatch, scene_name, w, h, spp, mb, grec):
