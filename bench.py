@@ -234,7 +234,8 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         samples = W * H * SPP * MB * args.steps
         value = samples / elapsed / 1e6
-        # roofline of the dominant kernel (rt_render_kernel), per launch
+        # roofline of the dominant kernel (the sorted kernel; the BVH refill
+        # kernel for the stress scene), per launch
         units = my_rows * W * SPP  # pixel-passes in one launch on this rank
         alg_bytes = units * BYTES_PER_PIXEL_PASS
         achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
@@ -268,7 +269,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (round(traffic["hbm_bytes_per_launch"]) if traffic else None),
-                         "kernel": "rt_render_sorted_kernel",
+                         "kernel": "rt_render_bvh_refill_kernel" if scene_key == "stress" else "rt_render_sorted_kernel",
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "bytes_per_unit": BYTES_PER_PIXEL_PASS, "units_per_launch": units},
         }
