@@ -1133,8 +1133,12 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
 #endif  // RT_TU_BVH
 
 // ---- launchers (host side) ------------------------------------------------
+// launch-order feedback applies to grids of more than RT_ORDER_MIN_GEN
+// generations of resident groups: 1.5 -> 1.1 turns it on for the c3 1/4
+// shard (1.32 generations: 0.297 -> 0.285 ms, two rounds, tools/shard_sweep.py;
+// c2 / c3 / c4 at the other shard sizes unchanged within noise)
 #ifndef RT_ORDER_MIN_GEN
-#define RT_ORDER_MIN_GEN 1.5
+#define RT_ORDER_MIN_GEN 1.1
 #endif
 // launch-order feedback: the grid of the last launch that sorted its
 // tile-group costs into group_order (0 = none; the context resets it before
