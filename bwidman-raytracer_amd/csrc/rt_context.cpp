@@ -284,7 +284,7 @@ void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_
     q[3] = d;
     for (int k = 0; k < nv; k++) {
         V3 in = cross(n, e[k]);  // Intersection.cuh:125-127
-        float* r = q + 4 + 6 * k;
+        float* r = q + RT_POLY_EDGES + 6 * k;
         r[0] = v[k].x;
         r[1] = v[k].y;
         r[2] = v[k].z;
@@ -1014,7 +1014,7 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             }
             for (int a = 0; a < 3; a++) upd(nm, rec[a]);
             for (int k = 0; k < nv; k++)  // {v_k[3], in_k[3]} from float 4 on
-                for (int a = 0; a < 3; a++) upd(im, rec[4 + 6 * k + 3 + a]);
+                for (int a = 0; a < 3; a++) upd(im, rec[RT_POLY_EDGES + 6 * k + 3 + a]);
         };
         for (int i = 0; i < nt; i++) polyb(s->triangles[i].vertices, 3, h.data() + off_tri + (size_t)i * RT_TRI_FLOATS);
         for (int i = 0; i < nq; i++) polyb(s->quads[i].vertices, 4, h.data() + off_quad + (size_t)i * RT_QUAD_FLOATS);
@@ -1185,10 +1185,16 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
                     src = h.data() + off_quad + (size_t)idx * RT_QUAD_FLOATS;
                 }
                 // {key, record...} (rt_layout.h): kind = key & 3, the id
-                // follows from the index
+                // follows from the index; polygons as {n, d, edges} without
+                // the cull sphere wherever the compiled record keeps it
                 const int key = RT_KEY(kind, idx);
                 std::memcpy(&r[0], &key, 4);
-                std::memcpy(&r[1], src, (size_t)nf * sizeof(float));
+                if (kind == 0) {
+                    std::memcpy(&r[1], src, (size_t)nf * sizeof(float));
+                } else {
+                    std::memcpy(&r[1], src, 4 * sizeof(float));
+                    std::memcpy(&r[5], src + RT_POLY_EDGES, (size_t)(kind == 2 ? 18 : 24) * sizeof(float));
+                }
             }
         }
     }

@@ -35,6 +35,7 @@
 #define RT_QUAD_FLOATS 32
 #define RT_TRI_CULL 24   // offset of the cull sphere in a triangle record
 #define RT_QUAD_CULL 28
+#define RT_POLY_EDGES 4  // offset of {v0, in0, v1, in1, ...} in a polygon record
 #define RT_LEAF_FLOATS 32  // BVH leaf record: RT_KEY + the record without its cull sphere (<= 28 floats)
 #ifndef RT_HIT_FLOATS
 #define RT_HIT_FLOATS 16

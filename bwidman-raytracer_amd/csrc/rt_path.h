@@ -412,7 +412,7 @@ RT_HD void polygon_test(const rt_kparams& K, cfloat_ptr q, int nv, f3 o, f3 d, i
         if (plane_hit && !(t <= RT_NEAR_ZERO || t > best_t)) {
             RT_BRANCH_COUNT(K, 3);
             f3 P = add(o, scale(t, d));
-            if (polygon_edges(q + 4, nv, P)) {
+            if (polygon_edges(q + RT_POLY_EDGES, nv, P)) {
                 best_t = t;
                 best_id = id;
             }
