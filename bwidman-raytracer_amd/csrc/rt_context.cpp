@@ -28,7 +28,7 @@
 #include "rt_layout.h"
 
 size_t rt_render_rec_floats(const rt_kparams& K);
-bool rt_render_wants_global_records(const rt_kparams& K);
+bool rt_render_wants_global_records(const rt_kparams& K, int num_cus);
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req, bool bvh_refill,
                             hipStream_t stream);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
@@ -1509,7 +1509,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     K.refill = c->refill > 0 ? c->refill : small ? RT_REFILL_SMALL : RT_REFILL;
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
-    if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K)))) {
+    if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K, c->num_cus)))) {
         const int rc = ensure_buf(c, c->rec, rt_render_rec_floats(K) * sizeof(float));
         if (rc) return rc;
         K.rec = (float*)c->rec.p;

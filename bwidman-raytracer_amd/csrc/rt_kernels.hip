@@ -1305,11 +1305,19 @@ hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_
 // Launch policy for the sorted kernel's record stack: global memory when the
 // LDS stack (3 dwords per level per lane) would hold the brute-force kernel
 // below RT_WAVES_PER_EU waves per SIMD, i.e. deep paths.  Measured: config
-// 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms; config 3 (maxBounces
-// 4, 6 waves with LDS records) 0.91 ms vs 0.95 in global memory; the BVH
-// kernel (VGPR-bound at 5 waves) 245 vs 255 ms, so it keeps LDS records.
+// 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms; the BVH kernel
+// (VGPR-bound at 5 waves) 245 vs 255 ms, so it keeps LDS records.
+// Also when global records let more 256-lane groups reside per CU (runtime
+// occupancy of both instantiations) and the frame runs at least
+// RT_GREC_MIN_GEN generations of them: config 3 (maxBounces 4) 6 -> 7
+// waves/SIMD, 0.816 -> 0.801 ms (three alternating runs); its row shards of
+// 1/2 .. 1/16 (1.1 - 2.3 generations) lose 2 - 7 % with global records and
+// config 2 gains no group, so both keep LDS records
+#ifndef RT_GREC_MIN_GEN
+#define RT_GREC_MIN_GEN 3.0
+#endif
 size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted);
-bool rt_render_wants_global_records(const rt_kparams& K) {
+bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
     if (K.bvh_nodes || K.max_bounces <= 0) return false;
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
@@ -1317,7 +1325,18 @@ bool rt_render_wants_global_records(const rt_kparams& K) {
     L.rec = nullptr;
     const size_t lds = rt_render_lds_bytes(L, 256, hit_lds, true);
     const long groups = (long)(160 * 1024) / (long)(lds ? lds : 1);  // 256-lane groups per CU: 1 wave per SIMD each
-    return groups < RT_WAVES_PER_EU;
+    if (groups < RT_WAVES_PER_EU) return true;
+    // resident 256-lane groups per CU with LDS / global records
+    L.rec = reinterpret_cast<float*>(&L);  // any non-null: the global-record LDS size
+    const size_t lds_g = rt_render_lds_bytes(L, 256, hit_lds, true);
+    int occ_l = 0, occ_g = 0;
+    const void* kl = hit_lds ? kernel_ptr<256, true, true, false, false>() : kernel_ptr<256, false, true, false, false>();
+    const void* kg = hit_lds ? kernel_ptr<256, true, true, false, true>() : kernel_ptr<256, false, true, false, true>();
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_l, kl, 256, lds) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_g, kg, 256, lds_g) != hipSuccess || occ_g <= occ_l)
+        return false;
+    const double gens = (double)((long)K.rows * K.width) / (256.0 * occ_g * (num_cus > 0 ? num_cus : 1));
+    return gens >= RT_GREC_MIN_GEN;
 }
 
 // Floats of a global-memory record stack for one launch: 3 planes per level
@@ -1361,7 +1380,11 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     simple = simple || K.spp_inner > 1;
     if (K.bvh_nodes && bvh_refill && !simple && block_req == 0) return rt_launch_render_bvh_refill(K, num_cus, stream);
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+#ifdef RT_NO_HIT_LDS  // A/B builds: hit table read from global memory
+    const bool hit_lds = false;
+#else
     const bool hit_lds = !K.bvh_nodes && (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
+#endif
     const bool small_block = (size_t)3 * (K.max_bounces + 1) * 256 * sizeof(float) > 49152;
     const int block = small_block ? 64 : 256;
     const size_t lds = rt_render_lds_bytes(K, block, hit_lds, !simple);
