@@ -180,13 +180,7 @@ __device__ __forceinline__ void store_pixel(const rt_kparams& K, long npix, cons
     if (K.rgba) K.rgba[p] = tone_map(s.ax, s.ay, s.az, s.frame - 1u);
 }
 
-// Folds levels depth-1 .. 0 of the LDS record stack into L (in/out).
-// `rs`: distance between levels (BLOCK in LDS, the grid's lanes in global memory)
-__device__ __forceinline__ void fold_records(const int* rec_code, const float* rec_k, const float* rec_c, int rs,
-                                             int depth, const float* hit_tab, float& lx, float& ly, float& lz) {
-    for (int l = depth - 1; l >= 0; --l)
-        fold_level(rec_code[l * rs], rec_k[l * rs], rec_c[l * rs], hit_tab, lx, ly, lz);
-}
+typedef __attribute__((address_space(3))) float lds_float;
 
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
@@ -525,21 +519,18 @@ rt_render_sorted_kernel(rt_kparams K) {
     // the path in the round it is made, so it is folded straight from the
     // lane's own task slot (fields 4..6, free once the result is taken)
     const int levels = K.max_bounces;
-    // record stack: LDS [field][level][lane]; GREC: only the shallow levels
-    // 0 .. LL-1 in LDS, the deep ones (rarely reached) in global memory in
-    // the same layout over the grid's lanes (stride RS), so LDS leaves room
-    // for RT_GREC_WAVES waves and few records ever leave the CU
+    // record stack: LDS [level][field][lane] (a level's three fields BLOCK
+    // dwords apart: one per-lane address, the fields as immediate offsets);
+    // GREC: only the shallow levels 0 .. LL-1 in LDS, the deep ones (rarely
+    // reached) in global memory, [group][level - LL][field][lane] (each
+    // group's records contiguous and coalesced), so LDS leaves room for
+    // RT_GREC_WAVES waves and few records ever leave the CU
     const int LL = GREC ? (levels < RT_GREC_LDS_LEVELS ? levels : RT_GREC_LDS_LEVELS) : levels;
-    const int RS = GREC ? K.rec_stride : BLOCK;
-    int* rec_code = reinterpret_cast<int*>(rec_base) + tid;
-    float* rec_k = rec_base + LL * BLOCK + tid;
-    float* rec_c = rec_base + 2 * LL * BLOCK + tid;
-    // global levels LL .. levels-1 only: plane (l - LL) of each field
+    // (an LDS-address-space pointer: 32-bit address arithmetic, no 64-bit
+    // base held across the loop)
+    lds_float* rec = (lds_float*)(rec_base + tid);
     const int GL = levels - LL;
-    float* grec_mem = GREC ? K.rec + (long)blockIdx.x * BLOCK : rec_base;
-    int* grec_code = reinterpret_cast<int*>(grec_mem) + tid;
-    float* grec_k = grec_mem + GL * RS + tid;
-    float* grec_c = grec_mem + 2 * GL * RS + tid;
+    float* grec = GREC ? K.rec + (long)blockIdx.x * 3 * GL * BLOCK + tid : rec_base;
     float* slots = rec_base + 3 * LL * BLOCK;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
     // counters[0..3]: queue fronts/backs (2 parities)
@@ -581,10 +572,14 @@ rt_render_sorted_kernel(rt_kparams K) {
             fold_level(__float_as_int(SLOT(6, slot)), SLOT(4, slot), SLOT(5, slot), hit_tab, lx, ly, lz);
         const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
         if (GREC)
-            for (int l = nrec - 1; l >= LL; --l)
-                fold_level(grec_code[(l - LL) * RS], grec_k[(l - LL) * RS], grec_c[(l - LL) * RS], hit_tab, lx, ly,
-                           lz);
-        fold_records(rec_code, rec_k, rec_c, BLOCK, nrec < LL ? nrec : LL, hit_tab, lx, ly, lz);
+            for (int l = nrec - 1; l >= LL; --l) {
+                const float* r = grec + 3 * (l - LL) * BLOCK;
+                fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+            }
+        for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
+            const lds_float* r = rec + 3 * l * BLOCK;
+            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+        }
         if (px.frame == 1u) {
             px.ax = 0.0f;
             px.ay = 0.0f;
@@ -775,14 +770,16 @@ rt_render_sorted_kernel(rt_kparams K) {
                 const float kspec = task == T_SPEC ? RES(3, slot) : 0.0f;
                 const float cosang = dot(d, hn);  // cosAngle, Main.cu:264
                 if (depth < K.max_bounces) {
-                    if (!GREC || depth < LL) {
-                        rec_code[depth * BLOCK] = code;
-                        rec_k[depth * BLOCK] = kspec;
-                        rec_c[depth * BLOCK] = cosang;
+                    if (!GREC || depth < LL) {  // (separate stores: LDS and global address spaces)
+                        lds_float* r = rec + 3 * depth * BLOCK;
+                        r[0] = __int_as_float(code);
+                        r[BLOCK] = kspec;
+                        r[2 * BLOCK] = cosang;
                     } else {
-                        grec_code[(depth - LL) * RS] = code;
-                        grec_k[(depth - LL) * RS] = kspec;
-                        grec_c[(depth - LL) * RS] = cosang;
+                        float* r = grec + 3 * (depth - LL) * BLOCK;
+                        r[0] = __int_as_float(code);
+                        r[BLOCK] = kspec;
+                        r[2 * BLOCK] = cosang;
                     }
                     has_ray = true;  // from the hit point o along d
                 } else {  // next query would exceed maxBounces (Main.cu:210): the path ends
@@ -1339,10 +1336,10 @@ bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
     return gens >= RT_GREC_MIN_GEN;
 }
 
-// Floats of a global-memory record stack for one launch: 3 planes per level
+// Floats of a global-memory record stack for one launch: 3 dwords per level
 // kept in global memory (levels RT_GREC_LDS_LEVELS .. max_bounces-1; the
-// shallow ones stay in LDS) over the grid's lanes (the grid covers every work
-// item, rounded up to the largest workgroup).  At least one float, so a
+// shallow ones stay in LDS) per lane of the grid (the grid covers every work
+// item, rounded up to the largest workgroup), [group][level][field][lane].  At least one float, so a
 // forced global-record launch with no global level still gets a buffer.
 size_t rt_render_rec_floats(const rt_kparams& K) {
     long nitems = (long)K.rows * K.width;

@@ -99,10 +99,11 @@ struct rt_kparams {
     // cull_dmax (no polygon test can overflow) may skip a polygon's exact test
     float cull_omax;
     float cull_dmax;
-    // recursion record stack in global memory (sorted kernel, deep paths):
-    // levels 0 .. RT_GREC_LDS_LEVELS-1 stay in LDS, the deeper ones take
-    // 3 * (max_bounces - RT_GREC_LDS_LEVELS) planes of rec_stride floats
-    // ([field][level - RT_GREC_LDS_LEVELS][lane]); null = all records in LDS
+    // recursion record stack in global memory (sorted kernel, deep paths and
+    // full frames): levels 0 .. RT_GREC_LDS_LEVELS-1 stay in LDS, the deeper
+    // ones take 3 * (max_bounces - RT_GREC_LDS_LEVELS) floats per lane of the
+    // grid, [group][level - RT_GREC_LDS_LEVELS][field][lane]; null = all
+    // records in LDS
     float* rec;
     int rec_stride;             // lanes in the grid (set by the launcher)
     // launch-order feedback (sorted kernel): workgroup g renders tile-group
