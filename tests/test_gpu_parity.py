@@ -761,9 +761,11 @@ def test_launch_order_feedback(bwrt_lib, oracle, monkeypatch, scene_name, w, h, 
     launch records its tile-groups' durations and the next launch starts the
     most expensive first): the first render runs in blockIdx order, the
     following ones reordered — every one equals the oracle bit for bit, and
-    a progressive continuation under the new order does too.  The grec case
-    is config 4's product path (maxBounces 6: global-memory records, levels
-    2-5 outside LDS) reordered."""
+    a progressive continuation under the new order does too.  The 07 1080p
+    maxBounces-4 case is config 3's product path (the launch policy's
+    global-memory records on a multi-generation frame: level 2-3 outside
+    LDS, 7 resident groups per CU); the grec case is config 4's (maxBounces
+    6: levels 2-5 outside LDS) reordered."""
     scene = scenes.SCENES[scene_name]()
     st = oracle.OracleState(w, h)
     oracle.render(scene, st, spp, mb, first_frame=1)
