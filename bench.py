@@ -159,6 +159,11 @@ def main():
     if len(hip_libs) != 1:
         print(f"warning: {len(hip_libs)} HIP runtimes loaded: {hip_libs}", file=sys.stderr)
     r = Renderer(dev_index, lib=lib)
+    # no per-launch start marker inside the library (a marker packet the GPU
+    # drains between two launches: 5-7 us per step, tools/ev_ab.sh); the bench
+    # brackets its whole timed region with one event pair instead
+    # (BENCH_KTIMING=1: library timing on, for that A/B)
+    r.set_kernel_timing(os.environ.get("BENCH_KTIMING") == "1")
     scene = scenes.SCENES[scene_key]()
     r.set_scene(scene)
     plan = ShardPlan(H, world, rank)
@@ -187,18 +192,14 @@ def main():
     params = r.params(W, H, SPP, MB, first_frame=1, row_offset=plan.row_offset, row_stride=plan.row_stride)
     counter = [0]
 
-    def step(ev=None):
+    def step():
         b = counter[0] % nbuf
         counter[0] += 1
         local_img = local_imgs[b]
         if overlap:
             stream.wait_event(ev_sent[b])  # no-op until the event is first recorded
-        if ev is not None:
-            ev[0].record(stream)
         r.render_device(params, local_img.data_ptr() if world > 1 else full_img.data_ptr(),
                         stream.cuda_stream)
-        if ev is not None:
-            ev[1].record(stream)
         if world > 1:
             ev_rendered[b].record(stream)
             with torch.cuda.stream(comm):
@@ -211,21 +212,26 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    # HIP events on the launch stream bracket the K timed launches (one pair:
+    # events between the steps would put marker packets, ~5 us each, between
+    # the launches); the average launch = their span / K, which also covers
+    # the order-sort kernel and the launch gaps of each step
+    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
+    ev_start.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev_end.record(stream)
     t_issued = time.perf_counter()  # host time to enqueue the steps (must stay below the GPU time)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in events]
-    t = torch.tensor([elapsed, sum(kern_ms) / len(kern_ms), t_issued - t0], dtype=torch.float64, device=dev)
+    kern_avg = ev_start.elapsed_time(ev_end) / args.steps
+    t = torch.tensor([elapsed, kern_avg, t_issued - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_avg_ms, issue_s = float(t[0]), float(t[1]), float(t[2])

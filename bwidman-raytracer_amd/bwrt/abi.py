@@ -117,6 +117,7 @@ def _proto(lib):
         "rt_synchronize": (C.c_int, [vp]),
         "rt_render_multi": (C.c_int, [P(vp), C.c_int, C.c_int, C.c_int, C.c_int, vp]),
         "rt_last_kernel_ms": (C.c_float, [vp]),
+        "rt_set_kernel_timing": (C.c_int, [vp, C.c_int]),
         "rt_shard_rows": (C.c_int, [C.c_int, C.c_int, C.c_int]),
         "rt_deinterleave_rows_device": (C.c_int, [vp, vp, vp, C.c_int, C.c_int, C.c_int,
                                                   C.c_int, vp]),

@@ -155,6 +155,10 @@ class Renderer:
     def last_kernel_ms(self) -> float:
         return self.lib.rt_last_kernel_ms(self.ctx)
 
+    def set_kernel_timing(self, enable: bool):
+        """Per-launch timing events for last_kernel_ms (rt_set_kernel_timing)."""
+        self._check(self.lib.rt_set_kernel_timing(self.ctx, int(bool(enable))))
+
     def deinterleave_device(self, gathered_ptr, image_ptr, width, height, shards, rows_per_shard,
                             stream_ptr=None):
         self._check(self.lib.rt_deinterleave_rows_device(self.ctx, gathered_ptr, image_ptr, width,

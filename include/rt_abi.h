@@ -311,8 +311,19 @@ RT_API int rt_render_multi(rt_context* const* ctxs, int n, int width, int height
                            uint8_t* rgba_out);
 
 /* Duration (ms, HIP events on the launch stream) of the last render kernel
- * launch; -1 when unavailable.  Synchronises on that launch's end event. */
+ * launch; -1 when unavailable (no render yet, or kernel timing off).
+ * Synchronises on that launch's end event. */
 RT_API float rt_last_kernel_ms(rt_context* ctx);
+
+/* Per-launch kernel timing (default on): every render records a start event
+ * before its kernels; its end event (recorded either way: later calls are
+ * ordered after it) closes the interval rt_last_kernel_ms reports.  Each event
+ * is a marker packet the GPU drains between two launches (MI355X, config 3:
+ * the start marker costs 5-7 us per launch, ~1 %; tools/ev_ab.sh,
+ * profiles/r03d/launch_events/).  Off, rt_last_kernel_ms returns -1.  The
+ * reference times nothing on the device (it prints host-side FPS,
+ * Main.cu:486-495). */
+RT_API int rt_set_kernel_timing(rt_context* ctx, int enable);
 
 /* Number of pixel rows in the shard (row_offset, row_stride) of `height`. */
 RT_API int rt_shard_rows(int height, int row_offset, int row_stride);

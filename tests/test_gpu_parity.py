@@ -479,6 +479,37 @@ def test_render_device_into_torch_buffer(gpu, oracle):
     assert gpu.last_kernel_ms() > 0
 
 
+def test_kernel_timing_off_and_on(gpu, oracle):
+    """rt_set_kernel_timing: the launch's start / end events ride on the
+    kernels' dispatch packets; with timing off rt_last_kernel_ms is -1 (no
+    stale value), the render and its ordering event are unchanged (a host
+    render on the context's stream after a device render on a torch stream
+    continues the state in order), and timing on again gives durations."""
+    import torch
+    s = scenes.scene_07()
+    gpu.set_scene(s)
+    w, h, mb = 320, 180, 4
+    gpu.init_rand(w, h)
+    st = oracle.OracleState(w, h)
+    buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.Stream()
+    try:
+        gpu.render(w, h, 1, mb, first_frame=1)
+        assert gpu.last_kernel_ms() > 0
+        gpu.set_kernel_timing(False)
+        assert gpu.last_kernel_ms() == -1.0
+        gpu.render_device(gpu.params(w, h, 2, mb, first_frame=2), buf.data_ptr(), stream.cuda_stream)
+        assert gpu.last_kernel_ms() == -1.0
+        img = gpu.render(w, h, 2, mb, first_frame=4)  # waits for the torch-stream render
+        want = oracle.render(s, st, 5, mb, first_frame=1)
+        assert np.array_equal(img, want)
+        gpu.set_kernel_timing(True)
+        gpu.render(w, h, 1, mb, first_frame=6)
+        assert gpu.last_kernel_ms() > 0
+    finally:
+        gpu.set_kernel_timing(True)
+
+
 def test_state_writes_wait_for_device_render(gpu, oracle):
     """rt_set_scene / rt_init_rand / rt_set_state right after an asynchronous
     rt_render_device on a torch stream must not overwrite the scene or the
