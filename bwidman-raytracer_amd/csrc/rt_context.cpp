@@ -135,6 +135,7 @@ struct rt_context {
     size_t host_rgba_bytes = 0;
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
     int tile_w = -1;             // BWRT_TILE: wave tile width (0 = linear order; -1 = launch policy)
+    int tile_sq = 0;             // BWRT_TILE_SQ: a 4-wave group's tiles as 2 x 2 (experiment)
     int leaf_batch = -1;         // BWRT_LEAF_BATCH: BVH refill kernel leaf-batch threshold (-1 = launch policy)
     int refill = -1;             // BWRT_REFILL: BVH refill kernel refill threshold (-1 = launch policy)
     unsigned frame = 1;
@@ -850,6 +851,7 @@ int rt_create(int device, rt_context** out) {
         const int t = std::atoi(tw);
         if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
     }
+    if (const char* g = std::getenv("BWRT_TILE_SQ")) c->tile_sq = std::atoi(g) != 0;
     if (const char* g = std::getenv("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
     if (const char* g = std::getenv("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = std::getenv("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
@@ -1501,13 +1503,18 @@ static int cpu_render(rt_context* c, const rt_render_params* p, int threads, uin
 }
 
 static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, int samples) {
-    // wave tiles: 16 x 4 pixels; on small shards (one rank of a multi-GPU
+    // wave tiles: 8 x 8 pixels; on small shards (one rank of a multi-GPU
     // frame, below 1024 pixels per CU) 32 x 2 (config 3 at 1/8: 0.249 ->
-    // 0.244 ms; full frames: 16 x 4 0.871 vs 32 x 2 0.877 ms); BVH scenes
-    // 8 x 8 (4 x 16 on small shards): squarer tiles keep a wave's rays closer
-    // together in the tree (config 5: 170.4 -> 167.7 ms; at 1/8 38.5 -> 35.2)
+    // 0.244 ms); BVH scenes 4 x 16 on small shards: squarer tiles keep a
+    // wave's rays closer together (config 5: 170.4 -> 167.7 ms; at 1/8 38.5 ->
+    // 35.2).  Full brute-force frames took 16 x 4 until late in round 3; with
+    // the kernel of then, 8 x 8 is ahead (bench kernel average, config 3,
+    // three alternating runs: 0.7495 / 0.7535 / 0.7497 vs 0.7579 / 0.7616 /
+    // 0.7559 ms; c2 -3 %, c4 5.51 vs 5.53 ms; 1/2 shard -2 %, 1/4 flat;
+    // profiles/r03e/c3_knobs.txt, profiles/r03e/tiles/)
     const bool small = (long)K.rows * K.width <= (long)c->num_cus * 1024;
-    K.tile_w = c->tile_w >= 0 ? c->tile_w : K.bvh_nodes ? (small ? 4 : 8) : (small ? 32 : 16);
+    K.tile_w = c->tile_w >= 0 ? c->tile_w : K.bvh_nodes ? (small ? 4 : 8) : (small ? 32 : 8);
+    K.tile_sq = c->tile_sq;
     // BVH refill kernel: test the parked leaves once this many of a wave's 64
     // lanes are ready; small shards (every wave resident at once, the frame
     // ends with the slowest waves) batch later
@@ -1537,7 +1544,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     // launch-order feedback: room for a grid of 64-lane groups over the
     // padded wave tiles (any block size needs fewer groups)
     if (c->order_feedback && !c->simple) {
-        const size_t cap = ((size_t)K.width + 64) * ((size_t)K.rows + 64) / 64 + 1;
+        const size_t cap = ((size_t)K.width + 128) * ((size_t)K.rows + 128) / 64 + 1;  // tiles padded to 2 x 2
         const void* before = c->gorder.p;
         int rc = ensure_buf(c, c->gcost, cap * sizeof(unsigned));
         if (!rc) rc = ensure_buf(c, c->gorder, cap * sizeof(int));

@@ -142,11 +142,21 @@ __device__ __forceinline__ void load_pixel(const rt_kparams& K, long npix, long 
 // wave) covering a tile_w x (64/tile_w) pixel tile, tiles row-major over the
 // shard; tile_w = 0 keeps the linear order (item = pixel).  Square-ish tiles
 // keep a wave's rays spatially coherent (a pixel-scrambled order costs +45 %).
-__device__ __forceinline__ long items_of(const rt_kparams& K, long npix) {
-    if (K.tile_w <= 0) return npix;
+// tile_sq: every 4 consecutive waves form a 2 x 2 block of tiles (a 4-wave
+// group then covers a square-ish patch), the tile grid padded to even sizes
+__host__ __device__ inline long launch_items(const rt_kparams& K) {
+    if (K.tile_w <= 0) return (long)K.rows * K.width;
     const int tw = K.tile_w, th = 64 / K.tile_w;
-    const long tiles_x = (K.width + tw - 1) / tw, tiles_y = (K.rows + th - 1) / th;
+    long tiles_x = (K.width + tw - 1) / tw, tiles_y = (K.rows + th - 1) / th;
+    if (K.tile_sq) {
+        tiles_x += tiles_x & 1;
+        tiles_y += tiles_y & 1;
+    }
     return tiles_x * tiles_y * 64;
+}
+
+__device__ __forceinline__ long items_of(const rt_kparams& K, long npix) {
+    return K.tile_w <= 0 ? npix : launch_items(K);
 }
 
 __device__ __forceinline__ long item_to_pixel(const rt_kparams& K, long npix, long w) {
@@ -155,8 +165,17 @@ __device__ __forceinline__ long item_to_pixel(const rt_kparams& K, long npix, lo
     const long tiles_x = (K.width + tw - 1) / tw;
     const long wave = w >> 6;
     const int l = (int)(w & 63);
-    const long x = (wave % tiles_x) * tw + (l % tw);
-    const long j = (wave / tiles_x) * th + (l / tw);
+    long tx, ty;
+    if (K.tile_sq) {
+        const long sx = (tiles_x + 1) >> 1, sw = wave >> 2;
+        tx = (sw % sx) * 2 + (wave & 1);
+        ty = (sw / sx) * 2 + ((wave >> 1) & 1);
+    } else {
+        tx = wave % tiles_x;
+        ty = wave / tiles_x;
+    }
+    const long x = tx * tw + (l % tw);
+    const long j = ty * th + (l / tw);
     if (x >= K.width || j >= K.rows) return npix;
     return j * K.width + x;
 }
@@ -1153,11 +1172,7 @@ void* kernel_ptr() {
 template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC = false>
 hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
     rt_kparams K = K0;
-    long nitems = (long)K.rows * K.width;
-    if (K.tile_w > 0) {
-        const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
-        nitems = tiles_x * tiles_y * 64;
-    }
+    const long nitems = launch_items(K);
     long grid = (nitems + BLOCK - 1) / BLOCK;  // streaming needs a resident grid only
     if (grid_mult > 0 && !SORTED) {  // persistent (simple kernel): grid_mult x resident groups per CU x CUs
         int per_cu = 0;
@@ -1226,11 +1241,7 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
 hipError_t rt_launch_render_bvh_refill(const rt_kparams& K0, int num_cus, hipStream_t s) {
     constexpr int BLOCK = 64;
     rt_kparams K = K0;
-    long nitems = (long)K.rows * K.width;
-    if (K.tile_w > 0) {
-        const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
-        nitems = tiles_x * tiles_y * 64;
-    }
+    const long nitems = launch_items(K);
     const long grid = (nitems + BLOCK - 1) / BLOCK < 1 ? 1 : (nitems + BLOCK - 1) / BLOCK;
     const size_t lds = (size_t)3 * (K.max_bounces + 1) * BLOCK * sizeof(float);
     // launch-order feedback (as launch_render): only for grids of more than
@@ -1342,11 +1353,7 @@ bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
 // item, rounded up to the largest workgroup), [group][level][field][lane].  At least one float, so a
 // forced global-record launch with no global level still gets a buffer.
 size_t rt_render_rec_floats(const rt_kparams& K) {
-    long nitems = (long)K.rows * K.width;
-    if (K.tile_w > 0) {
-        const long tiles_x = (K.width + K.tile_w - 1) / K.tile_w, tiles_y = (K.rows + 64 / K.tile_w - 1) / (64 / K.tile_w);
-        nitems = tiles_x * tiles_y * 64;
-    }
+    const long nitems = launch_items(K);
     const int lds_levels = K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS;
     const size_t planes = (size_t)3 * (K.max_bounces - lds_levels);
     return planes ? planes * (size_t)((nitems + 255) / 256 * 256) : 1;

@@ -69,6 +69,7 @@ struct rt_kparams {
     unsigned* rgba;             // rows*width (may be null)
     unsigned long long* stamps; // diagnostic builds (-DRT_STAMPS) only: per-phase cycle sums
     int tile_w;                 // wave tile width in pixels (1..64, power of 2); 0 = linear order
+    int tile_sq;                // waves of a 4-wave group as 2 x 2 tiles (else 4 tiles in a row)
     // bounding-volume hierarchy over spheres/triangles/quads (large scenes;
     // null = brute-force loop): 8 threaded node arrays (one per ray-direction
     // octant, bit a = d[a] < 0; bvh_order_stride floats apart).  Node: 8
