@@ -129,6 +129,15 @@ struct rt_context {
     // launch and the order sorted from them, valid for a grid of order_n groups
     DevBuf gcost, gorder;
     long order_n = 0;
+    // re-sort the launch order every order_period-th launch (BWRT_ORDER_PERIOD;
+    // a grid without an order is always sorted): the per-group costs follow
+    // the image, so a kept order is as good as a fresh one, and the sort
+    // kernel plus its launch gap cost ~8 us per launch.  Config 3 bench kernel
+    // average, three alternating runs: every launch 0.7567 / 0.7543 / 0.7535,
+    // every 4th 0.7479 / 0.7461 / 0.7476, every 16th 0.7462 / 0.7430 / 0.7469,
+    // never again 0.7451 / 0.7458 / 0.7484 ms (profiles/r03f/order_period_ab.txt)
+    int order_period = 16;
+    unsigned long long launches = 0;
     bool order_feedback = true;  // BWRT_ORDER=0: blockIdx order
     int grec = -1;  // BWRT_GREC: 1 / 0 force global / LDS records; -1 = launch policy
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
@@ -857,6 +866,7 @@ int rt_create(int device, rt_context** out) {
     if (const char* g = std::getenv("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = std::getenv("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
     if (const char* g = std::getenv("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
+    if (const char* g = std::getenv("BWRT_ORDER_PERIOD")) c->order_period = std::max(std::atoi(g), 1);
     *out = c;
     return RT_OK;
 }
@@ -1554,6 +1564,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.group_order = (int*)c->gorder.p;
         K.order_n = c->order_n;
         K.order_cap = (long)(c->gorder.bytes / sizeof(int));
+        K.order_sort = c->launches % (unsigned long long)c->order_period == 0;
     }
     // renders continue each other's RNG / frameSum state: a launch on a
     // different stream than the previous one waits for it (no host sync)
@@ -1566,6 +1577,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     if (c->ktiming) HIP_TRY(c, hipEventRecord(c->ev0, s));
     hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, s);
     if (e == hipSuccess && rt_order_groups_last > 0) c->order_n = rt_order_groups_last;
+    c->launches++;
     if (gtimes && stamps) {
         std::vector<unsigned long long> h(NGT);
         (void)hipMemcpyAsync(h.data(), stamps, NGT * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);

@@ -1224,7 +1224,8 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     else
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && feedback) {
+    // the sort runs when asked, and always for a grid without an order yet
+    if (e == hipSuccess && feedback && (K0.order_sort || K0.order_n != grid)) {
         e = rt_launch_order_groups(K0.group_cost, K0.group_order, grid, stream);
         if (e == hipSuccess) rt_order_groups_last = grid;
     }
@@ -1270,7 +1271,7 @@ hipError_t rt_launch_render_bvh_refill(const rt_kparams& K0, int num_cus, hipStr
     else
         hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && feedback) {
+    if (e == hipSuccess && feedback && (K0.order_sort || K0.order_n != grid)) {
         e = rt_launch_order_groups(K0.group_cost, K0.group_order, grid, s);
         if (e == hipSuccess) rt_order_groups_last = grid;
     }

@@ -117,6 +117,7 @@ struct rt_kparams {
     unsigned* group_cost;
     long order_n;               // grid the current group_order was built for (0 = none)
     long order_cap;             // capacity of group_order / group_cost
+    int order_sort;             // sort this launch's costs into group_order (else the order is kept)
     int leaf_batch;             // BVH refill kernel: leaf tests once this many lanes are ready
     int refill;                 // BVH refill kernel: new rays once this many of 64 (relative) wait
     // samplesPerPixel (Main.cu:27, 296-299): paths traced per frame from the

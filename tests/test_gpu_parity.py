@@ -755,8 +755,8 @@ def test_launch_order_feedback_bvh_refill(bwrt_lib, monkeypatch):
     """Launch-order feedback in the BVH ray-refill kernel (config 5's
     product path): the stress scene at 1920x1080, 2 spp, 8 bounces — a grid
     of 32,400 single-wave groups, several resident generations — rendered
-    four times (blockIdx order, then each launch in the order sorted from the
-    last) and once as a continuation; every image, frameSum and RNG state
+    four times (blockIdx order, then in orders re-sorted every 2nd launch)
+    and once as a continuation; every image, frameSum and RNG state
     equals the product's CPU fallback (itself pinned to the oracle,
     tests/test_cpu_fallback.py; the brute-force oracle would need minutes)."""
     from bwrt import Renderer
@@ -768,7 +768,7 @@ def test_launch_order_feedback_bvh_refill(bwrt_lib, monkeypatch):
         want_rng, _ = c.get_state(1080, 1920)
         cont = c.render(1920, 1080, 1, 8, want_accum=True)
         cont_rng, _ = c.get_state(1080, 1920)
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1, BWRT_ORDER_PERIOD=2)
     try:
         r.set_scene(s)
         for _ in range(4):
@@ -800,11 +800,14 @@ def test_launch_order_feedback(bwrt_lib, oracle, monkeypatch, scene_name, w, h, 
     scene = scenes.SCENES[scene_name]()
     st = oracle.OracleState(w, h)
     oracle.render(scene, st, spp, mb, first_frame=1)
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1, BWRT_GREC=grec) if grec else \
-        _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1, BWRT_ORDER_PERIOD=2, BWRT_GREC=grec) if grec else \
+        _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1, BWRT_ORDER_PERIOD=2)
     try:
         r.set_scene(scene)
-        for _ in range(4):  # blockIdx order first, then each launch in the order sorted from the last
+        # blockIdx order first, then orders re-sorted every 2nd launch (launch 1
+        # keeps launch 0's sort, launch 2 sorts again; the product re-sorts
+        # every 16th, rt_context.cpp order_period)
+        for _ in range(4):
             r.init_rand(w, h)
             img = r.render(w, h, spp, mb, first_frame=1)
             assert np.array_equal(img, st.rgba)
