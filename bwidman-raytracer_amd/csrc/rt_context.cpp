@@ -135,7 +135,8 @@ struct rt_context {
     // kernel plus its launch gap cost ~8 us per launch.  Config 3 bench kernel
     // average, three alternating runs: every launch 0.7567 / 0.7543 / 0.7535,
     // every 4th 0.7479 / 0.7461 / 0.7476, every 16th 0.7462 / 0.7430 / 0.7469,
-    // never again 0.7451 / 0.7458 / 0.7484 ms (profiles/r03f/order_period_ab.txt)
+    // never again 0.7451 / 0.7458 / 0.7484 ms (profiles/r03f/order_period_ab.txt);
+    // config 2 0.1503 / 0.1515 vs 0.1555 / 0.1565, config 4 5.50 vs 5.52 ms
     int order_period = 16;
     unsigned long long launches = 0;
     bool order_feedback = true;  // BWRT_ORDER=0: blockIdx order
@@ -1564,7 +1565,11 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.group_order = (int*)c->gorder.p;
         K.order_n = c->order_n;
         K.order_cap = (long)(c->gorder.bytes / sizeof(int));
-        K.order_sort = c->launches % (unsigned long long)c->order_period == 0;
+        // BVH scenes re-sort every launch: their order keeps improving when
+        // sorted from costs measured under the previous order (config 5: 85.8
+        // / 86.3 / 86.1 ms every launch vs 86.7 / 87.0 / 87.0 every 16th), and
+        // the sort is 6.5 us of an 86 ms frame (profiles/r03g/order_period_configs_ab.txt)
+        K.order_sort = K.bvh_nodes || c->launches % (unsigned long long)c->order_period == 0;
     }
     // renders continue each other's RNG / frameSum state: a launch on a
     // different stream than the previous one waits for it (no host sync)
