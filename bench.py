@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(scenes.CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true",
-                    help="rank 0 re-renders the whole frame on its GPU alone and checks the gathered image")
+                    help="also at N = 1: re-render from fresh seeds and check the frame against the CPU fallback's "
+                         "rows (N > 1 always checks the gathered frame against rank 0's single-GPU render)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: gather each frame before the next render starts (no frame pipelining)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -181,10 +182,13 @@ def main():
     # the gather's landing buffers exist on the root only
     gathered = ([torch.empty((world, rows_per * W), dtype=torch.int32, device=dev) for _ in range(nbuf)]
                 if world > 1 and rank == 0 else [None] * nbuf)
-    # a dedicated (non-null) stream: the kernel, its timing events and the
-    # RCCL gather are all ordered on it (NULL would mean the context's own
-    # stream in the C ABI)
-    stream = torch.cuda.Stream(dev)
+    # the context's own stream (rt_get_stream), wrapped for torch: the
+    # kernel, the bench's timing events and the RCCL gather are all ordered
+    # on it, and renders on the context's stream defer the library's end
+    # event, so back-to-back steps carry no marker packet between them
+    # (BENCH_CALLER_STREAM=1: a torch-created stream instead, for that A/B)
+    stream = (torch.cuda.Stream(dev) if os.environ.get("BENCH_CALLER_STREAM") == "1"
+              else torch.cuda.ExternalStream(r.stream_handle(), device=dev))
     comm = torch.cuda.Stream(dev) if overlap else stream
     torch.cuda.set_stream(stream)
     ev_rendered = [torch.cuda.Event() for _ in range(nbuf)]
@@ -230,11 +234,62 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_avg = ev_start.elapsed_time(ev_end) / args.steps
-    t = torch.tensor([elapsed, kern_avg, t_issued - t0], dtype=torch.float64, device=dev)
+    kern_span = ev_start.elapsed_time(ev_end) / args.steps
+    t = torch.tensor([elapsed, kern_span, t_issued - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_avg_ms, issue_s = float(t[0]), float(t[1]), float(t[2])
+    kernel_timing = "event pair around the timed launches on the render stream, / steps"
+    if world > 1:
+        # the timed region's span on the render stream also holds its waits
+        # for the gather stream (and, with --no-overlap, the gather itself):
+        # the render kernel's own time comes from render-only launches after
+        # the timed region (same shard, no gather), max over ranks
+        kreps = min(args.steps, 10)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(kreps):
+            r.render_device(params, local_imgs[0].data_ptr(), stream.cuda_stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        k = torch.tensor([e0.elapsed_time(e1) / kreps], dtype=torch.float64, device=dev)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kern_avg_ms = float(k[0])
+        kernel_timing = f"render-only pass of {kreps} launches after the timed region (no gather), max over ranks"
+
+    # parity of the measured path: N > 1 always (the sharded + gathered frame
+    # from fresh seeds against rank 0 rendering the whole frame alone); N = 1
+    # with --verify (a fresh frame against the CPU fallback on a row sample)
+    verified, verify_how = None, None
+    if world > 1:
+        r.init_rand(W, H, plan.row_offset, plan.row_stride)
+        step()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            got = full_img.cpu()
+            solo_r = Renderer(dev_index, lib=lib)
+            solo_r.set_scene(scene)
+            solo = torch.empty(H * W, dtype=torch.int32, device=dev)
+            solo_r.init_rand(W, H)
+            solo_r.render_device(solo_r.params(W, H, SPP, MB, first_frame=1), solo.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            solo_r.close()
+            verified = bool(torch.equal(got, solo.cpu()))
+            verify_how = f"{world}-rank gathered frame (fresh y*W+x seeds) vs rank 0's 1-GPU render, bit for bit"
+    elif args.verify:
+        verify_rows = CPU_SAMPLE_ROW_STRIDE.get(args.config, 1) * 8
+        with Renderer.cpu(0, lib=lib) as c, Renderer(dev_index, lib=lib) as g:
+            c.set_scene(scene)
+            g.set_scene(scene)
+            c.init_rand(W, H, 0, verify_rows)
+            g.init_rand(W, H, 0, verify_rows)
+            a = c.render(W, H, SPP, MB, first_frame=1, row_stride=verify_rows)
+            b = g.render(W, H, SPP, MB, first_frame=1, row_stride=verify_rows)
+        verified = bool((a == b).all())
+        verify_how = f"rows y = 0 mod {verify_rows} (fresh seeds): GPU vs the CPU fallback, bit for bit"
 
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
@@ -265,8 +320,13 @@ def main():
                        "scene": scene_key, "width": W, "height": H, "spp": SPP, "max_bounces": MB,
                        "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} gather" if world > 1 else "")
                        + (" (frames pipelined: gather of frame k overlaps render of k+1)" if overlap else "")},
+            "world_size": world,
+            "backend": (("rccl" if backend == "nccl" else backend) if world > 1 else None),
+            "verified": verified,
+            "verify": verify_how,
             "ms_per_frame": round(ms_step, 4),
             "kernel_ms_avg": round(kern_avg_ms, 4),
+            "kernel_timing": kernel_timing,
             # host time to enqueue one step (render + gather calls), max over ranks
             "host_issue_ms_per_step": round(issue_s / args.steps * 1e3, 4),
             "queries_per_frame": QUERIES_PER_FRAME.get(args.config),
@@ -299,28 +359,21 @@ def main():
                 check.set_scene(scene)
                 out["cpu_baseline"] = cpu_baseline(lib, args.config, scene_key, W, H, SPP, MB, args.cpu_threads,
                                                    gpu_renderer=check)
+            if out["verified"] is None:
+                out["verified"] = out["cpu_baseline"]["bit_exact_vs_gpu"]
+                out["verify"] = "the CPU baseline's sample: GPU vs the CPU fallback from the same seeds, bit for bit"
         print(json.dumps(out), flush=True)
-    if args.verify:
-        # one more sharded + gathered frame from freshly seeded RNG streams
-        # must equal rank 0 rendering the whole frame alone
-        r.init_rand(W, H, plan.row_offset, plan.row_stride)
-        step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        if rank == 0:
-            got = full_img.cpu()
-            solo = torch.empty(H * W, dtype=torch.int32, device=dev)
-            r.init_rand(W, H)
-            r.render_device(r.params(W, H, SPP, MB, first_frame=1), solo.data_ptr(), stream.cuda_stream)
-            torch.cuda.synchronize(dev)
-            same = torch.equal(got, solo.cpu())
-            print(f"verify: {world}-rank gathered frame {'==' if same else '!='} 1-GPU frame", flush=True)
-            if not same:
-                raise SystemExit(1)
+    ok = torch.tensor([0 if verified is False else 1], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.broadcast(ok, 0)
+    torch.cuda.synchronize(dev)
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))  # the context's stream goes with it
     r.close()
     if world > 1:
         dist.destroy_process_group()
+    if int(ok[0]) == 0 or (rank == 0 and world == 1 and out.get("verified") is False):
+        print("verify FAILED: the measured path's frame differs", file=sys.stderr, flush=True)
+        raise SystemExit(1)
 
 
 if __name__ == "__main__":

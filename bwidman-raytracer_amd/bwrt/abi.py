@@ -115,6 +115,7 @@ def _proto(lib):
         "rt_render_ex": (C.c_int, [vp, P(RenderParams), vp, vp]),
         "rt_render_device": (C.c_int, [vp, P(RenderParams), vp, vp]),
         "rt_synchronize": (C.c_int, [vp]),
+        "rt_get_stream": (vp, [vp]),
         "rt_render_multi": (C.c_int, [P(vp), C.c_int, C.c_int, C.c_int, C.c_int, vp]),
         "rt_last_kernel_ms": (C.c_float, [vp]),
         "rt_set_kernel_timing": (C.c_int, [vp, C.c_int]),

@@ -152,6 +152,11 @@ class Renderer:
     def synchronize(self):
         self._check(self.lib.rt_synchronize(self.ctx))
 
+    def stream_handle(self) -> int:
+        """The context's own hipStream_t (rt_get_stream): renders on it defer
+        their end event (no marker packet between back-to-back renders)."""
+        return self.lib.rt_get_stream(self.ctx) or 0
+
     def last_kernel_ms(self) -> float:
         return self.lib.rt_last_kernel_ms(self.ctx)
 

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <xmmintrin.h>
 #include <vector>
 
 #include "../../include/rt_abi.h"
@@ -91,6 +92,9 @@ struct rt_context {
     hipEvent_t ev_render = nullptr;
     hipStream_t render_stream = nullptr;
     bool render_recorded = false;
+    // the last render ran on the context's own stream and its end event is
+    // not recorded yet (rt_get_stream): flush_render() records it on demand
+    bool render_pending = false;
     // end of the last de-interleave on a caller's stream (rt_synchronize)
     hipEvent_t ev_aux = nullptr;
     bool aux_recorded = false;
@@ -138,6 +142,9 @@ struct rt_context {
     // never again 0.7451 / 0.7458 / 0.7484 ms (profiles/r03f/order_period_ab.txt);
     // config 2 0.1503 / 0.1515 vs 0.1555 / 0.1565, config 4 5.50 vs 5.52 ms
     int order_period = 16;
+    // the kept order was measured on another image (new scene, camera or
+    // shard): the next launch re-sorts its costs whatever the period
+    bool order_stale = true;
     unsigned long long launches = 0;
     bool order_feedback = true;  // BWRT_ORDER=0: blockIdx order
     int grec = -1;  // BWRT_GREC: 1 / 0 force global / LDS records; -1 = launch policy
@@ -148,12 +155,45 @@ struct rt_context {
     int tile_sq = 0;             // BWRT_TILE_SQ: a 4-wave group's tiles as 2 x 2 (experiment)
     int leaf_batch = -1;         // BWRT_LEAF_BATCH: BVH refill kernel leaf-batch threshold (-1 = launch policy)
     int refill = -1;             // BWRT_REFILL: BVH refill kernel refill threshold (-1 = launch policy)
+    int tail_n = -1;             // BWRT_TAIL: sorted-kernel tail-mode threshold (-1 = launch policy)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
     int spp_inner = 1;  // samplesPerPixel, Main.cu:27
 };
 
 namespace {
+
+// Tuning and diagnostic knobs (BWRT_BLOCK, BWRT_TILE, BWRT_GREC, BWRT_TAIL,
+// BWRT_ORDER*, BWRT_BVH_*, BWRT_STAMPS, ...; listed in rt_abi.h) are read
+// only when the process sets BWRT_TUNING=1: a default context always takes
+// the measured launch policy, whatever else the environment holds.
+// IEEE float state for the library's host-side float work (scene compile,
+// camera set-up, controls): round to nearest, no FTZ / DAZ, whatever the
+// calling thread holds (a -ffast-math library or torch.set_flush_denormal
+// may have set them), restored on return — the GPU keeps f32 denormals and
+// the compiled scene must not depend on the caller
+struct HostFpEnv {
+    unsigned saved;
+    HostFpEnv() : saved(_mm_getcsr()) {
+        _mm_setcsr((saved & ~(_MM_ROUND_MASK | _MM_FLUSH_ZERO_MASK | 0x0040u)) | _MM_ROUND_NEAREST);  // 0x40 = DAZ
+    }
+    ~HostFpEnv() { _mm_setcsr(saved); }
+};
+
+const char* tuning_env(const char* name) {
+    const char* t = std::getenv("BWRT_TUNING");
+    return t && std::strcmp(t, "1") == 0 ? std::getenv(name) : nullptr;
+}
+
+// Record the end event of a render launched on the context's own stream
+// whose recording was deferred (see launch)
+hipError_t flush_render(rt_context* c) {
+    if (!c->render_pending) return hipSuccess;
+    c->render_pending = false;
+    const hipError_t e = hipEventRecord(c->ev_render, c->stream);
+    if (e == hipSuccess) c->render_recorded = true;
+    return e;
+}
 
 int fail(rt_context* c, int code, const char* fmt, ...) {
     if (c) {
@@ -190,7 +230,9 @@ void free_buf(DevBuf& b) {
 // (its event, recorded on whatever stream it ran on).  Work on c->stream is
 // already ordered by the stream itself.
 int quiesce(rt_context* c) {
-    if (c->cpu || !c->render_recorded) return RT_OK;
+    if (c->cpu) return RT_OK;
+    HIP_TRY(c, flush_render(c));
+    if (!c->render_recorded) return RT_OK;
     HIP_TRY(c, hipEventSynchronize(c->ev_render));
     return RT_OK;
 }
@@ -854,20 +896,21 @@ int rt_create(int device, rt_context** out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = prop.multiProcessorCount;
-    if (const char* gm = std::getenv("BWRT_GRID_MULT")) c->grid_mult = std::atoi(gm);
-    if (const char* kk = std::getenv("BWRT_KERNEL")) c->simple = std::strcmp(kk, "simple") == 0;
-    if (const char* bk = std::getenv("BWRT_BLOCK")) c->block = std::atoi(bk);
-    if (const char* tw = std::getenv("BWRT_TILE")) {
+    if (const char* gm = tuning_env("BWRT_GRID_MULT")) c->grid_mult = std::atoi(gm);
+    if (const char* kk = tuning_env("BWRT_KERNEL")) c->simple = std::strcmp(kk, "simple") == 0;
+    if (const char* bk = tuning_env("BWRT_BLOCK")) c->block = std::atoi(bk);
+    if (const char* tw = tuning_env("BWRT_TILE")) {
         const int t = std::atoi(tw);
         if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
     }
-    if (const char* g = std::getenv("BWRT_TILE_SQ")) c->tile_sq = std::atoi(g) != 0;
-    if (const char* g = std::getenv("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
-    if (const char* g = std::getenv("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
-    if (const char* g = std::getenv("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
-    if (const char* g = std::getenv("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
-    if (const char* g = std::getenv("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
-    if (const char* g = std::getenv("BWRT_ORDER_PERIOD")) c->order_period = std::max(std::atoi(g), 1);
+    if (const char* g = tuning_env("BWRT_TILE_SQ")) c->tile_sq = std::atoi(g) != 0;
+    if (const char* g = tuning_env("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
+    if (const char* g = tuning_env("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
+    if (const char* g = tuning_env("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
+    if (const char* g = tuning_env("BWRT_TAIL")) c->tail_n = std::min(std::max(std::atoi(g), 0), RT_TAIL_MAX);
+    if (const char* g = tuning_env("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
+    if (const char* g = tuning_env("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
+    if (const char* g = tuning_env("BWRT_ORDER_PERIOD")) c->order_period = std::max(std::atoi(g), 1);
     *out = c;
     return RT_OK;
 }
@@ -917,6 +960,7 @@ void rt_destroy(rt_context* c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->render_pending = false;  // its launch is done: the stream is synchronised
     if (c->render_recorded) (void)hipEventSynchronize(c->ev_render);
     if (c->aux_recorded) (void)hipEventSynchronize(c->ev_aux);
     free_buf(c->scene_buf);
@@ -935,6 +979,7 @@ void rt_destroy(rt_context* c) {
 }
 
 int rt_set_scene(rt_context* c, const rt_scene* s) {
+    const HostFpEnv fp;
     if (!c || !s) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
     if (s->sphere_count < 0 || s->plane_count < 0 || s->triangle_count < 0 || s->quad_count < 0)
         return fail(c, RT_ERR_INVALID_ARGUMENT, "negative primitive count");
@@ -994,7 +1039,7 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     for (int i = 0; i < nq; i++)
         for (int k = 0; k < 4; k++) grow(s->quads[i].vertices[k], 0.0);
     scale *= 2.0;
-    if (!std::isfinite(scale) || scale > 1e30 || std::getenv("BWRT_NO_CULL")) scale = INFINITY;
+    if (!std::isfinite(scale) || scale > 1e30 || tuning_env("BWRT_NO_CULL")) scale = INFINITY;
     c->cull_omax = std::isfinite(scale) ? (float)scale : -1.0f;  // -1: no ray is culled
     for (int i = 0; i < nt; i++, id++)
         compile_polygon(h.data() + off_tri + (size_t)i * RT_TRI_FLOATS, hit + (size_t)id * RT_HIT_FLOATS,
@@ -1058,7 +1103,7 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     size_t off_bvh = 0, off_bvh_prims = 0, off_bvh16 = 0;
     {
         int bvh_min = 64;
-        if (const char* e = std::getenv("BWRT_BVH_MIN")) bvh_min = std::atoi(e);
+        if (const char* e = tuning_env("BWRT_BVH_MIN")) bvh_min = std::atoi(e);
         const int nb = ns + nt + nq;
         if (nb > 0 && nb >= bvh_min) {
             // leaf encoding: 24-bit index of a leaf's first primitive record
@@ -1089,12 +1134,12 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             B.tree.reserve(2 * (size_t)nb);
             // leaf = (count << 24) | first in an int: count <= 127 keeps the sign
             // bit clear (a negative value means "internal node" to the kernels)
-            if (const char* e = std::getenv("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 127);
-            if (const char* e = std::getenv("BWRT_BVH_CT")) B.trav_cost = (float)std::atof(e);
+            if (const char* e = tuning_env("BWRT_BVH_LEAF")) B.max_leaf = std::min(std::max(std::atoi(e), 1), 127);
+            if (const char* e = tuning_env("BWRT_BVH_CT")) B.trav_cost = (float)std::atof(e);
             // spatial splits (BWRT_BVH_SBVH=0: object splits only), references
             // up to BWRT_BVH_REFS x the primitives (default 2)
             bool sbvh = true;
-            if (const char* e = std::getenv("BWRT_BVH_SBVH")) sbvh = std::atoi(e) != 0;
+            if (const char* e = tuning_env("BWRT_BVH_SBVH")) sbvh = std::atoi(e) != 0;
             if (sbvh) {
                 B.geo.assign((size_t)12 * (ns + np + nt + nq), 0.0);
                 B.geo_nv.assign((size_t)(ns + np + nt + nq), 0);
@@ -1140,8 +1185,8 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
                 for (int i = 0; i < nt; i++) polyref(ns + np + i, s->triangles[i].vertices, 3);
                 for (int i = 0; i < nq; i++) polyref(ns + np + nt + i, s->quads[i].vertices, 4);
                 double refs_x = 2.0;
-                if (const char* e = std::getenv("BWRT_BVH_REFS")) refs_x = std::atof(e);
-                if (const char* e = std::getenv("BWRT_BVH_ALPHA")) B.split_alpha = std::atof(e);
+                if (const char* e = tuning_env("BWRT_BVH_REFS")) refs_x = std::atof(e);
+                if (const char* e = tuning_env("BWRT_BVH_ALPHA")) B.split_alpha = std::atof(e);
                 B.root_area = BvhBuilder::darea(rlo, rhi);
                 B.ref_budget = (size_t)(refs_x * nb);
                 B.n_refs = (size_t)nb;
@@ -1164,9 +1209,9 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
                 for (int a = 0; a < 3; a++)
                     if (!(ext[a] < 0.5f * mx)) B.order_mask |= 1 << a;
             }
-            if (const char* e = std::getenv("BWRT_BVH_ORDER_MASK")) B.order_mask = std::atoi(e) & 7;
+            if (const char* e = tuning_env("BWRT_BVH_ORDER_MASK")) B.order_mask = std::atoi(e) & 7;
             B.finish();
-            if (std::getenv("BWRT_BVH_STATS")) {  // diagnostics (tests, tuning)
+            if (tuning_env("BWRT_BVH_STATS")) {  // diagnostics (tests, tuning)
                 long ax[3] = {0, 0, 0}, inner = 0;
                 for (const BvhNode& t : B.tree)
                     if (t.left >= 0) ax[t.axis]++, inner++;
@@ -1230,10 +1275,11 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     c->off_hit = off_hit;
     c->off_bvh = off_bvh;
     c->off_bvh_prims = off_bvh_prims;
-    c->off_bvh16 = std::getenv("BWRT_BVH_N16") && !std::atoi(std::getenv("BWRT_BVH_N16")) ? 0 : off_bvh16;
+    c->off_bvh16 = tuning_env("BWRT_BVH_N16") && !std::atoi(tuning_env("BWRT_BVH_N16")) ? 0 : off_bvh16;
     c->camera = s->camera;
     c->has_scene = true;
     c->frame = 1;
+    c->order_stale = true;
     return RT_OK;
 }
 
@@ -1241,6 +1287,7 @@ int rt_set_camera(rt_context* c, const rt_camera* cam) {
     if (!c || !cam) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
     c->camera = *cam;
     c->frame = 1;  // Controls.cuh: any movement sets accumulatedFrames = 1
+    c->order_stale = true;
     return RT_OK;
 }
 
@@ -1263,6 +1310,7 @@ int rt_get_camera(const rt_context* c, rt_camera* cam) {
 // vector (mat * vec = row dots, Math.cuh:144-150); position +/-= k * dir.
 int rt_apply_controls(rt_camera* cam, unsigned keys, float dt) {
     if (!cam) return RT_ERR_INVALID_ARGUMENT;
+    const HostFpEnv fp;
     const float move = 5 * dt;
     const float rot = 2 * dt;
     const float cy = cosf(cam->angle[0]), sy = sinf(cam->angle[0]);  // rotationMatrix3DY
@@ -1327,7 +1375,10 @@ int rt_apply_controls(rt_camera* cam, unsigned keys, float dt) {
 int rt_controls(rt_context* c, unsigned keys, float dt) {
     if (!c) return RT_ERR_INVALID_ARGUMENT;
     const int flags = rt_apply_controls(&c->camera, keys, dt);
-    if (flags > 0 && (flags & RT_CONTROLS_MOVED)) c->frame = 1;  // accumulatedFrames = 1
+    if (flags > 0 && (flags & RT_CONTROLS_MOVED)) {
+        c->frame = 1;  // accumulatedFrames = 1
+        c->order_stale = true;
+    }
     return flags;
 }
 
@@ -1410,10 +1461,12 @@ int rt_init_rand(rt_context* c, int width, int height, int row_offset, int row_s
     c->row_stride = row_stride;
     c->rows = rows;
     c->frame = 1;
+    c->order_stale = true;
     return RT_OK;
 }
 
 static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsigned& first) {
+    const HostFpEnv fp;
     if (!c || !p) return fail(c, RT_ERR_INVALID_ARGUMENT, "null argument");
     if (!c->has_scene) return fail(c, RT_ERR_NO_SCENE, "rt_set_scene() not called");
     const int stride = p->row_stride == 0 ? 1 : p->row_stride;
@@ -1531,6 +1584,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     // ends with the slowest waves) batch later
     K.leaf_batch = c->leaf_batch > 0 ? c->leaf_batch : small ? RT_LEAF_BATCH_SMALL : RT_LEAF_BATCH;
     K.refill = c->refill > 0 ? c->refill : small ? RT_REFILL_SMALL : RT_REFILL;
+    K.tail_n = c->tail_n >= 0 ? c->tail_n : RT_TAIL_N;
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
     if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K, c->num_cus)))) {
@@ -1539,13 +1593,13 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.rec = (float*)c->rec.p;
     }
     unsigned long long* stamps = nullptr;
-    const int NST = 32;  // 8 per-phase wave-cycle sums + utilisation / branch counters
-    if (std::getenv("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS)
+    const int NST = 40;  // 8 per-phase wave-cycle sums + utilisation / branch counters + tail
+    if (tuning_env("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS)
         if (hipMalloc(&stamps, NST * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemsetAsync(stamps, 0, NST * sizeof(unsigned long long), s);
         K.stamps = stamps;
     }
-    const char* gtimes = std::getenv("BWRT_GTIMES");  // diagnostic builds (-DRT_GTIMES): group times file
+    const char* gtimes = tuning_env("BWRT_GTIMES");  // diagnostic builds (-DRT_GTIMES): group times file
     const size_t NGT = (size_t)1 << 22;
     if (gtimes && !stamps) {
         if (hipMalloc(&stamps, NGT * sizeof(unsigned long long)) == hipSuccess)
@@ -1569,11 +1623,15 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         // sorted from costs measured under the previous order (config 5: 85.8
         // / 86.3 / 86.1 ms every launch vs 86.7 / 87.0 / 87.0 every 16th), and
         // the sort is 6.5 us of an 86 ms frame (profiles/r03g/order_period_configs_ab.txt)
-        K.order_sort = K.bvh_nodes || c->launches % (unsigned long long)c->order_period == 0;
+        K.order_sort = K.bvh_nodes || c->order_stale || c->launches % (unsigned long long)c->order_period == 0;
+        c->order_stale = false;
     }
     // renders continue each other's RNG / frameSum state: a launch on a
     // different stream than the previous one waits for it (no host sync)
-    if (c->render_stream && c->render_stream != s) HIP_TRY(c, hipStreamWaitEvent(s, c->ev_render, 0));
+    if (c->render_stream && c->render_stream != s) {
+        HIP_TRY(c, flush_render(c));
+        HIP_TRY(c, hipStreamWaitEvent(s, c->ev_render, 0));
+    }
     rt_order_groups_last = 0;
     // every event recorded here is a marker packet the GPU drains between two
     // renders (~5 us each on MI355X, tools/ev_ab.sh): the start marker only
@@ -1604,9 +1662,17 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         (void)hipFree(stamps);
     }
     if (e != hipSuccess) return hip_fail(c, e, "rt_render_kernel launch");
-    HIP_TRY(c, hipEventRecord(c->ev_render, s));
     c->render_stream = s;
-    c->render_recorded = true;
+    if (s == c->stream && !c->ktiming) {
+        // the context's own stream, which lives as long as the context: the
+        // end event is recorded only when a later call needs it (flush_render),
+        // so back-to-back renders carry no marker packet between them
+        c->render_pending = true;
+    } else {
+        c->render_pending = false;
+        HIP_TRY(c, hipEventRecord(c->ev_render, s));
+        c->render_recorded = true;
+    }
     c->timed = c->ktiming;
     c->frame = first + (unsigned)samples;  // Main.cu:480 accumulatedFrames++
     return RT_OK;
@@ -1737,10 +1803,13 @@ int rt_synchronize(rt_context* c) {
     if (c->cpu) return RT_OK;  // CPU renders are synchronous
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->render_pending = false;  // a deferred end event's launch is done too
     if (c->render_recorded) HIP_TRY(c, hipEventSynchronize(c->ev_render));
     if (c->aux_recorded) HIP_TRY(c, hipEventSynchronize(c->ev_aux));
     return RT_OK;
 }
+
+void* rt_get_stream(rt_context* c) { return c && !c->cpu ? (void*)c->stream : nullptr; }
 
 float rt_last_kernel_ms(rt_context* c) {
     if (c && c->cpu) return c->cpu_ms;

@@ -19,6 +19,8 @@
 // here (include/rt_abi.h).  A GPU context never falls back to it.
 #include <atomic>
 #include <thread>
+
+#include <xmmintrin.h>  // MXCSR
 #include <vector>
 
 #include "rt_path.h"
@@ -197,10 +199,17 @@ int rt_cpu_render(const rt_kparams& K, int threads) {
     if ((long)threads > chunks) threads = (int)(chunks > 0 ? chunks : 1);
     std::atomic<long> next(0);
     auto work = [&]() {
+        // IEEE float state for the whole render, whatever the calling thread
+        // holds (a -ffast-math library or torch.set_flush_denormal may have
+        // set FTZ / DAZ, and new threads inherit it): round to nearest, no
+        // denormal flushing — the GPU keeps f32 denormals — restored after
+        const unsigned saved = _mm_getcsr();
+        _mm_setcsr((saved & ~(_MM_ROUND_MASK | _MM_FLUSH_ZERO_MASK | 0x0040u)) | _MM_ROUND_NEAREST);  // 0x40 = DAZ
         for (long c = next.fetch_add(1); c < chunks; c = next.fetch_add(1)) {
             const long end = (c + 1) * kChunk < npix ? (c + 1) * kChunk : npix;
             for (long p = c * kChunk; p < end; p++) render_pixel(K, npix, p);
         }
+        _mm_setcsr(saved);
     };
     std::vector<std::thread> pool;
     pool.reserve((size_t)threads - 1);

@@ -206,6 +206,147 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
                                           __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
 
+// ---- diagnostics: RT_PHASE_TWICE = 1 / 2 / 3 / 4 runs the sorted kernel's
+// closest hit / RANDDIR task / SPEC task / path-end fold a second time on
+// opaque copies of its inputs (results kept alive, never used), so the PMC
+// deltas against the plain build (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU) are
+// that phase's VALU instructions and lane-cycles (tools/phase_lanes.sh)
+#ifndef RT_PHASE_TWICE
+#define RT_PHASE_TWICE 0
+#endif
+__device__ __forceinline__ float opq(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ f3 opq3(f3 v) { return mk(opq(v.x), opq(v.y), opq(v.z)); }
+__device__ __forceinline__ void keep(float x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void keep_i(int x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ Xorwow opq_rs(Xorwow r) {
+    Xorwow q;
+    q.d = __float_as_uint(opq(__uint_as_float(r.d)));
+    q.v0 = __float_as_uint(opq(__uint_as_float(r.v0)));
+    q.v1 = __float_as_uint(opq(__uint_as_float(r.v1)));
+    q.v2 = __float_as_uint(opq(__uint_as_float(r.v2)));
+    q.v3 = __float_as_uint(opq(__uint_as_float(r.v3)));
+    q.v4 = __float_as_uint(opq(__uint_as_float(r.v4)));
+    return q;
+}
+
+// ---- tail mode: one closest hit split over a segment of S lanes -----------
+// (S = 2, 4, 8 or 16 aligned lanes that hold the same ray).  Lane sl of the
+// segment tests primitives j = sl, sl + S, ... of the list [spheres, planes,
+// triangles, quads] with the reference's arithmetic (closest_hit_brute's
+// tests, records staged in LDS), keeping the best (t, RT_KEY) by key_accept;
+// the segment then reduces its lanes' bests with DPP (quad xor 1, quad xor 2,
+// row half-mirror, row mirror: every step stays inside an aligned segment).
+// The result is the minimum distance with ties to the largest key, which is
+// what the reference's interleaved `t > closest` loop (Main.cu:217-234)
+// returns for rays whose tests cannot produce a NaN distance (bvh_safe); the
+// caller sends the other rays through closest_hit_brute.
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4f lds_v4f;
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ void coop_pick(float& bt, int& bk, float t2, int k2) {
+    if (t2 < bt || (t2 == bt && k2 > bk)) {
+        bt = t2;
+        bk = k2;
+    }
+}
+
+template <int CTRL>
+__device__ __forceinline__ void coop_step(float& bt, int& bk) {
+    const float t2 = __int_as_float(dpp_i<CTRL>(__float_as_int(bt)));
+    const int k2 = dpp_i<CTRL>(bk);
+    coop_pick(bt, bk, t2, k2);
+}
+
+template <bool QUADS>
+__device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_float* sc, f3 o, f3 d, int sl, int S,
+                                                 float& best_t, int& best_id) {
+    const float a = dot(d, d);
+    const float a4 = 4.0f * a;
+    const float a2 = 2.0f * a;
+    const CullRay cr = cull_ray(K, o, d, a);
+    const int e_pln = K.n_sph, e_tri = e_pln + K.n_pln, e_quad = e_tri + K.n_tri;
+    const int n = QUADS ? e_quad + K.n_quad : e_quad;
+    const lds_float* pln = sc + RT_SPH_FLOATS * K.n_sph;
+    const lds_float* tri = pln + RT_PLN_FLOATS * K.n_pln;
+    const lds_float* quad = tri + RT_TRI_FLOATS * K.n_tri;
+    float bt = INFINITY;
+    int bk = -1;
+    for (int j = sl; j < n; j += S) {
+        float t = INFINITY;
+        int key = -1;
+        if (j < e_pln) {  // sphere j, Intersection.cuh:15-62 (closest_hit_brute's test)
+            const v4f s = *reinterpret_cast<const lds_v4f*>(sc + RT_SPH_FLOATS * j);
+            const f3 xp = mk(o.x - s.x, o.y - s.y, o.z - s.z);
+            const float b = 2.0f * dot(xp, d);
+            const float c = dot(xp, xp) - s.w;
+            const float disc = b * b - a4 * c;
+            if (!(disc < 0.0f) && !(b >= 0.0f && disc == disc && a2 > 0.0f)) {
+                t = (-b - rt_sqrt(disc)) / a2;
+                key = RT_KEY(0, j);
+            }
+        } else if (j < e_tri) {  // plane, Intersection.cuh:64-106
+            const int i = j - e_pln;
+            const v4f q = *reinterpret_cast<const lds_v4f*>(pln + RT_PLN_FLOATS * i);
+            const float nd = q.x * d.x + q.y * d.y + q.z * d.z;
+            if (!(fabsf(nd) < RT_NEAR_ZERO)) {
+                t = -((q.x * o.x + q.y * o.y + q.z * o.z) + q.w) / nd;
+                key = RT_KEY(1, i);
+            }
+        } else {  // triangle / quad, Intersection.cuh:108-173 (polygon_test)
+            const bool is_tri = !QUADS || j < e_quad;
+            const int i = is_tri ? j - e_tri : j - e_quad;
+            const int nv = is_tri ? 3 : 4;
+            const lds_float* q = is_tri ? tri + RT_TRI_FLOATS * i : quad + RT_QUAD_FLOATS * i;
+            const v4f cs = *reinterpret_cast<const lds_v4f*>(q + (is_tri ? RT_TRI_CULL : RT_QUAD_CULL));
+            const float wx = cs.x - o.x, wy = cs.y - o.y, wz = cs.z - o.z;
+            const float ww = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
+            const float pj = __builtin_fmaf(wx, d.x, __builtin_fmaf(wy, d.y, wz * d.z));
+            const bool cull = cr.ok && __builtin_fmaf(-pj, pj, ww * cr.a_k) > cs.w * cr.a;
+            if (!cull) {
+                const v4f pl = *reinterpret_cast<const lds_v4f*>(q);
+                const float nd = pl.x * d.x + pl.y * d.y + pl.z * d.z;
+                if (!(fabsf(nd) < RT_NEAR_ZERO)) {
+                    const float tp = -((pl.x * o.x + pl.y * o.y + pl.z * o.z) + pl.w) / nd;
+                    const int kp = RT_KEY(is_tri ? 2 : 3, i);
+                    if (key_accept(tp, kp, bt, bk)) {
+                        const f3 P = add(o, scale(tp, d));
+                        bool inside = true;
+                        for (int k = 0; k < 4; k++) {
+                            if (k < nv) {
+                                const lds_float* e = q + RT_POLY_EDGES + 6 * k;
+                                if (dot(mk(e[3], e[4], e[5]), sub(P, mk(e[0], e[1], e[2]))) < 0.0f) inside = false;
+                            }
+                        }
+                        if (inside) {
+                            t = tp;
+                            key = kp;
+                        }
+                    }
+                }
+            }
+        }
+        if (key >= 0 && key_accept(t, key, bt, bk)) {
+            bt = t;
+            bk = key;
+        }
+    }
+    if (S >= 2) coop_step<0xB1>(bt, bk);   // quad_perm [1,0,3,2]
+    if (S >= 4) coop_step<0x4E>(bt, bk);   // quad_perm [2,3,0,1]
+    if (S >= 8) coop_step<0x141>(bt, bk);  // row_half_mirror
+    if (S >= 16) coop_step<0x140>(bt, bk); // row_mirror
+    best_t = bt;
+    const int kind = bk & 3, idx = bk >> 2;
+    best_id = bk < 0 ? -1 : idx + (kind == 0 ? 0 : kind == 1 ? e_pln : kind == 2 ? e_tri : e_quad);
+}
+
 }  // namespace
 
 // LDS layout: [hit table, n_prim*12 floats, if HIT_LDS] then the record stack
@@ -236,6 +377,10 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 #endif
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
+#endif
+// tail mode of the sorted kernel compiled in (K.tail_n turns it on per launch)
+#ifndef RT_TAIL
+#define RT_TAIL 1
 #endif
 
 template <int BLOCK, bool HIT_LDS, bool BVH>
@@ -495,6 +640,189 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 #endif  // RT_TU_BVH
 
 
+
+// Tail mode of rt_render_sorted_kernel (see there): wave 0 finishes the
+// group's last `live` pixels from their hand-off records H; segments of S
+// lanes per pixel run its tasks redundantly and split its closest hits
+// (coop_closest_hit).  Not inlined (see the call).
+enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };  // a lane's next task
+template <int BLOCK, bool HIT_LDS, bool GREC, bool QUADS>
+__device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((address_space(4))) rt_kparams* kp_arg,
+                                                      int tail_live_arg) {
+    // everything uniform comes from the kernel-argument segment and the LDS
+    // base.  The arguments of a call arrive in VGPRs, so the pointer is made
+    // wave-uniform here (scalar loads of the scene and the parameters instead
+    // of per-lane vector loads; the hit table from LDS, not through flat
+    // loads).  The kernarg-segment intrinsic itself is valid in kernels only:
+    // in a callee it yields a null base
+    extern __shared__ float smem[];
+    const unsigned long long kpi = (unsigned long long)kp_arg;
+    const unsigned kp_lo = __builtin_amdgcn_readfirstlane((unsigned)kpi);
+    const unsigned kp_hi = __builtin_amdgcn_readfirstlane((unsigned)(kpi >> 32));
+    const __attribute__((address_space(4))) rt_kparams* kp =
+        (const __attribute__((address_space(4))) rt_kparams*)(((unsigned long long)kp_hi << 32) | kp_lo);
+    const rt_kparams& K = *(const rt_kparams*)kp;
+    const int tail_live = __builtin_amdgcn_readfirstlane(tail_live_arg);
+    const int tid = threadIdx.x;
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    const float* hit_tab = HIT_LDS ? smem : K.hit;
+    float* rec_base = HIT_LDS ? smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3) : smem;
+    const int levels = K.max_bounces;
+    const int LL = GREC ? (levels < RT_GREC_LDS_LEVELS ? levels : RT_GREC_LDS_LEVELS) : levels;
+    const lds_float* H = (const lds_float*)(rec_base + 3 * LL * BLOCK);
+    const lds_float* sc = H + RT_TAIL_FIELDS * RT_TAIL_MAX;
+    const long npix = (long)K.rows * K.width;
+    const int GL = K.max_bounces - LL;
+    const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
+    const f3 o = mk(0.0f, 0.0f, 0.0f), d = o, hn = o;
+    // segment size: 64 / (live pixels rounded up to a power of 2), at most 16
+    const int p2 = tail_live <= 1 ? 1 : 1 << (32 - __builtin_clz(tail_live - 1));
+    const int S = 64 / p2 < 16 ? 64 / p2 : 16;
+    const int seg = tid / S, sl = tid - seg * S;
+    bool live = seg < tail_live;
+    PixelState q;
+    int tmode = T_NONE, otid = 0;
+    f3 to = o, td = d, thn = hn;
+    int thid = 0, tdepth = 0;
+    if (live) {
+#define HR(f) H[(f) * RT_TAIL_MAX + seg]
+        q.p = __float_as_int(HR(0));
+        q.frame = __float_as_uint(HR(1));
+        q.passes_left = __float_as_int(HR(2));
+        q.ax = HR(3);
+        q.ay = HR(4);
+        q.az = HR(5);
+        q.d0 = mk(HR(6), HR(7), HR(8));
+        q.rs.d = __float_as_uint(HR(9));
+        q.rs.v0 = __float_as_uint(HR(10));
+        q.rs.v1 = __float_as_uint(HR(11));
+        q.rs.v2 = __float_as_uint(HR(12));
+        q.rs.v3 = __float_as_uint(HR(13));
+        q.rs.v4 = __float_as_uint(HR(14));
+        to = mk(HR(15), HR(16), HR(17));
+        td = mk(HR(18), HR(19), HR(20));
+        thn = mk(HR(21), HR(22), HR(23));
+        thid = __float_as_int(HR(24));
+        tdepth = __float_as_int(HR(25));
+        tmode = __float_as_int(HR(26));
+        otid = __float_as_int(HR(27));
+#undef HR
+    }
+    lds_float* trec = (lds_float*)(rec_base + otid);
+    float* tgrec = GREC ? K.rec + (long)blockIdx.x * 3 * GL * BLOCK + otid : rec_base;
+#ifdef RT_STAMPS
+    // diagnostic: K.stamps[32] tail wave-cycles, [33] tail rounds, [34]
+    // tail entries, [35] pixels handed over
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long st_rounds = 0;
+#endif
+    while (__any(live)) {
+#ifdef RT_STAMPS
+        st_rounds++;
+#endif
+        bool has_ray = false, tended = false;
+        int lcode = 0;
+        float lk = 0.0f, lc = 0.0f;
+        // the task of the round (T-phase): camera ray or bounce direction
+        if (live) {
+            if (tmode == T_REGEN) {  // Main.cu:290-292
+                const f3 r = random_direction(q.rs, q.d0);
+                td = normalize3(add(q.d0, scale(K.jitter, r)));
+                to = cam;
+                tdepth = 0;
+                has_ray = true;
+            } else {
+                float kspec = 0.0f;
+                int code = thid;
+                if (tmode == T_SPEC) {  // Main.cu:245-255
+                    const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * thid + 8);
+                    td = specular_scatter(q.rs, td, thn, h2.x, h2.z, h2.y, kspec);
+                    code = ~thid;
+                } else {  // diffuse, Main.cu:257-260
+                    td = random_direction(q.rs, thn);
+                }
+                const float cosang = dot(td, thn);  // cosAngle, Main.cu:264
+                if (tdepth < K.max_bounces) {
+                    if (!GREC || tdepth < LL) {
+                        lds_float* r = trec + 3 * tdepth * BLOCK;
+                        r[0] = __int_as_float(code);
+                        r[BLOCK] = kspec;
+                        r[2 * BLOCK] = cosang;
+                    } else {
+                        float* r = tgrec + 3 * (tdepth - LL) * BLOCK;
+                        r[0] = __int_as_float(code);
+                        r[BLOCK] = kspec;
+                        r[2 * BLOCK] = cosang;
+                    }
+                    has_ray = true;
+                } else {  // the deepest level (Main.cu:210): kept in registers
+                    lcode = code;
+                    lk = kspec;
+                    lc = cosang;
+                    tended = true;
+                }
+                tdepth++;
+            }
+        }
+        // closest hit (Main.cu:214-234), split over the segment
+        float t = INFINITY;
+        int id = -1;
+        if (has_ray) {
+            if (bvh_safe(K, to, td))
+                coop_closest_hit<QUADS>(K, sc, to, td, sl, S, t, id);
+            else  // NaN-capable tests: the reference's own loop order
+                closest_hit_brute<QUADS>(K, to, td, t, id);
+            if (id >= 0) {
+                const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
+                to = add(to, scale(t, td));
+                thn = mk(h0.x, h0.y, h0.z);
+                if (h0.w != 0.0f) thn = normalize3(sub(to, thn));
+                thid = id;
+                tmode = rand_range(q.rs, 1.0f) < RT_SPECULAR_CHANCE ? T_SPEC : T_DIFF;  // Main.cu:243
+            } else {
+                tended = true;
+            }
+        }
+        if (tended) {  // fold, accumulate (Main.cu:262-268, 299-304)
+            float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];
+            if (tdepth > K.max_bounces) fold_level(lcode, lk, lc, hit_tab, lx, ly, lz);
+            const int nrec = tdepth > K.max_bounces ? K.max_bounces : tdepth;
+            if (GREC)
+                for (int l = nrec - 1; l >= LL; --l) {
+                    const float* r = tgrec + 3 * (l - LL) * BLOCK;
+                    fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+                }
+            for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
+                const lds_float* r = trec + 3 * l * BLOCK;
+                fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+            }
+            if (q.frame == 1u) {
+                q.ax = 0.0f;
+                q.ay = 0.0f;
+                q.az = 0.0f;
+            }
+            q.ax = q.ax + lx;
+            q.ay = q.ay + ly;
+            q.az = q.az + lz;
+            q.frame++;
+            q.passes_left--;
+            tmode = q.passes_left > 0 ? T_REGEN : T_NONE;
+            if (tmode == T_NONE) {  // pixel done (every lane of the segment stores the same words)
+                store_pixel(K, npix, q);
+                live = false;
+            }
+        }
+    }
+#ifdef RT_STAMPS
+    if (tid == 0 && K.stamps) {
+        atomicAdd(&K.stamps[32], __builtin_amdgcn_s_memtime() - st_t0);
+        atomicAdd(&K.stamps[33], st_rounds);
+        atomicAdd(&K.stamps[34], 1ull);
+        atomicAdd(&K.stamps[35], (unsigned long long)tail_live);
+    }
+#endif
+}
+
 // ===========================================================================
 // Sorted task-queue megakernel (the product path).
 //
@@ -519,10 +847,8 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
 template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC && !BVH ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(!BVH && (GREC || RT_TAIL) ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
-    // a lane's next task: none (idle), camera ray, diffuse or specular bounce
-    enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -599,6 +925,23 @@ rt_render_sorted_kernel(rt_kparams K) {
             const lds_float* r = rec + 3 * l * BLOCK;
             fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
         }
+#if RT_PHASE_TWICE == 4
+        {
+            float mx = opq(K.bg[0]), my = opq(K.bg[1]), mz = opq(K.bg[2]);
+            if (depth > K.max_bounces)
+                fold_level(__float_as_int(opq(SLOT(6, slot))), opq(SLOT(4, slot)), opq(SLOT(5, slot)), hit_tab, mx, my, mz);
+            if (GREC)
+                for (int l = nrec - 1; l >= LL; --l) {
+                    const float* r = grec + 3 * (l - LL) * BLOCK;
+                    fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
+                }
+            for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
+                const lds_float* r = rec + 3 * l * BLOCK;
+                fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
+            }
+            keep(mx + my + mz);
+        }
+#endif
         if (px.frame == 1u) {
             px.ax = 0.0f;
             px.ay = 0.0f;
@@ -615,6 +958,9 @@ rt_render_sorted_kernel(rt_kparams K) {
         mode = px.passes_left > 0 ? T_REGEN : T_NONE;
     };
     bool ended = false;  // path ended this round: finish_path() once, after the I-phase
+    // tail mode (below the loop): live pixels of the group and this lane's
+    // hand-off index (-1: no live pixel)
+    int tail_live = 0, tail_c = -1;
 
 #ifdef RT_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -689,6 +1035,15 @@ rt_render_sorted_kernel(rt_kparams K) {
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
         if (nf + nb == 0) break;
+#if RT_TAIL
+        // few live pixels left (one per posted task; group-uniform): hand
+        // them to wave 0's tail loop below instead of running this round
+        if (!BVH && nf + nb <= K.tail_n) {
+            tail_live = nf + nb;
+            tail_c = slot < 0 ? -1 : slot < nf ? slot : nf + (BLOCK - 1 - slot);
+            break;
+        }
+#endif
 
         // ---- T-phase: execute slot `tid`
         {
@@ -720,12 +1075,29 @@ rt_render_sorted_kernel(rt_kparams K) {
                 int* rej_ptr = nullptr;
 #endif
                 if (do_front) {
+#if RT_PHASE_TWICE == 2
+                    {
+                        Xorwow r2 = opq_rs(rs);
+                        const f3 x = random_direction(r2, opq3(nrm));
+                        keep(x.x + x.y + x.z);
+                        keep_i((int)r2.v4);
+                    }
+#endif
                     r = random_direction(rs, nrm, rej_ptr);
                     if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
                 } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
                     float kspec;
+#if RT_PHASE_TWICE == 3
+                    {
+                        Xorwow r2 = opq_rs(rs);
+                        float k2;
+                        const f3 x = specular_scatter(r2, opq3(dd), opq3(nrm), opq(h2.x), opq(h2.z), opq(h2.y), k2);
+                        keep(x.x + x.y + x.z + k2);
+                        keep_i((int)r2.v4);
+                    }
+#endif
                     r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
                     RES(3, tid) = kspec;
                 }
@@ -826,6 +1198,15 @@ rt_render_sorted_kernel(rt_kparams K) {
             has_ray = false;
             float t;
             int id;
+#if RT_PHASE_TWICE == 1
+            {
+                float t2;
+                int id2;
+                closest_hit<BVH, QUADS>(K, opq3(o), opq3(d), t2, id2);
+                keep(t2);
+                keep_i(id2);
+            }
+#endif
             closest_hit<BVH, QUADS>(K, o, d, t, id);
             if (id >= 0) {
                 const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
@@ -846,6 +1227,63 @@ rt_render_sorted_kernel(rt_kparams K) {
         STAMP(6);
     }
     if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
+#if RT_TAIL
+    if (!BVH && tail_live > 0) {  // group-uniform
+        // ---- tail mode.  The group's few live pixels (each with its task of
+        // this round still to run) move to wave 0, which finishes them in a
+        // loop of its own: no barriers, no task slots, and each pixel held
+        // by a segment of S lanes that run its tasks redundantly (the same
+        // RNG stream, the same results) and split its closest hits.  The
+        // other waves leave.  Hand-off record [field][pixel] in the task-slot
+        // area (free: this round's slots are never executed), the scene's
+        // records behind it (the launcher checks that both fit).
+        lds_float* H = (lds_float*)slots;
+        lds_float* sc = H + RT_TAIL_FIELDS * RT_TAIL_MAX;
+        if (tail_c >= 0) {
+#define HW(f, v) H[(f) * RT_TAIL_MAX + tail_c] = (v)
+            HW(0, __int_as_float((int)px.p));
+            HW(1, __uint_as_float(px.frame));
+            HW(2, __int_as_float(px.passes_left));
+            HW(3, px.ax);
+            HW(4, px.ay);
+            HW(5, px.az);
+            HW(6, px.d0.x);
+            HW(7, px.d0.y);
+            HW(8, px.d0.z);
+            HW(9, __uint_as_float(px.rs.d));
+            HW(10, __uint_as_float(px.rs.v0));
+            HW(11, __uint_as_float(px.rs.v1));
+            HW(12, __uint_as_float(px.rs.v2));
+            HW(13, __uint_as_float(px.rs.v3));
+            HW(14, __uint_as_float(px.rs.v4));
+            HW(15, o.x);
+            HW(16, o.y);
+            HW(17, o.z);
+            HW(18, d.x);
+            HW(19, d.y);
+            HW(20, d.z);
+            HW(21, hn.x);
+            HW(22, hn.y);
+            HW(23, hn.z);
+            HW(24, __int_as_float(hid));
+            HW(25, __int_as_float(depth));
+            HW(26, __int_as_float(mode));
+            HW(27, __int_as_float(tid));
+#undef HW
+        }
+        const int nsc = RT_SPH_FLOATS * K.n_sph + RT_PLN_FLOATS * K.n_pln + RT_TRI_FLOATS * K.n_tri +
+                        (QUADS ? RT_QUAD_FLOATS * K.n_quad : 0);
+        for (int i = tid; i < nsc; i += BLOCK) sc[i] = K.sph[i];  // sph | pln | tri | quad are contiguous
+        __syncthreads();
+        if (tid < 64) {
+            // a call, not inlined: the tail's registers stay out of the main
+            // loop's allocation (inlined, it cost the global-record kernel 6
+            // spilled VGPRs and 29 more spilled SGPRs)
+            rt_tail_run<BLOCK, HIT_LDS, GREC, QUADS>(
+                (const __attribute__((address_space(4))) rt_kparams*)__builtin_amdgcn_kernarg_segment_ptr(), tail_live);
+        }
+    }
+#endif
     // the loop exit is group-uniform (the round that posts no task), so one
     // lane's clock after the loop closes the group's span
     if (ORDER && tid == 0) {
@@ -1185,6 +1623,14 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     if (grid < 1) grid = 1;
     K.rec_stride = (int)(grid * BLOCK);
+    // tail mode: brute-force scenes whose compiled records fit in the task-slot
+    // area beside the hand-off record
+    if (K.tail_n > 0) {
+        const long nsc = (long)RT_SPH_FLOATS * K.n_sph + (long)RT_PLN_FLOATS * K.n_pln +
+                         (long)RT_TRI_FLOATS * K.n_tri + (long)RT_QUAD_FLOATS * K.n_quad;
+        if (!SORTED || BVH || !RT_TAIL || (long)RT_TAIL_FIELDS * RT_TAIL_MAX + nsc > 13L * BLOCK) K.tail_n = 0;
+        if (K.tail_n > RT_TAIL_MAX) K.tail_n = RT_TAIL_MAX;
+    }
     // launch-order feedback: only where the sorted grid covers every item
     // once (group g <-> tile-group g) and the buffers hold the grid
     // and only where the grid runs in more than RT_ORDER_MIN_GEN generations

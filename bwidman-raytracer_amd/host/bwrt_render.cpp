@@ -219,8 +219,12 @@ int main(int argc, char** argv) {
         delta += frame_s;
         frame_count += n;
         if (delta > 1.0 || done == frames || quit) {  // Main.cu:486-495
+            // Main.cu:491 prints accumulatedFrames * samplesPerPixel after
+            // accumulatedFrames++ and controls(): the next frame's index
+            // (rendered frames since the last reset + 1), which is
+            // rt_frame_counter() after rt_controls()
             std::printf("FPS: %d | Samples: %u | kernel %.3f ms\n", (int)(frame_count / delta),
-                        (rt_frame_counter(ctx) - 1) * (unsigned)spp, rt_last_kernel_ms(ctx));
+                        rt_frame_counter(ctx) * (unsigned)spp, rt_last_kernel_ms(ctx));
             delta = 0.0;
             frame_count = 0;
         }

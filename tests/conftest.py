@@ -18,6 +18,10 @@ for p in (REPO, os.path.join(REPO, "bwidman-raytracer_amd"), os.path.join(REPO, 
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# the tests force launch knobs (BWRT_BLOCK, BWRT_GREC, BWRT_TAIL, ...): the
+# library reads them only under BWRT_TUNING=1 (test_host_io checks the gate)
+os.environ.setdefault("BWRT_TUNING", "1")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libbwrt.so / HIP)")

@@ -249,11 +249,62 @@ def test_cli_config1_on_cpu_fallback(bwrt_lib, oracle, tmp_path):
     r = subprocess.run([cli, "--cpu", "2", "--scene", "01", "--width", "256", "--height", "256", "--frames", "1",
                         "--max-bounces", "1", "--out", str(png)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert "CPU fallback: 2 threads" in r.stdout and "Samples: 1" in r.stdout
+    # "Samples:" = accumulatedFrames * samplesPerPixel after accumulatedFrames++ (Main.cu:480, 491)
+    assert "CPU fallback: 2 threads" in r.stdout and "Samples: 2" in r.stdout
     st = oracle.render_image(scenes.scene_01(), 256, 256, 1, 1)
     assert np.array_equal(np.asarray(Image.open(png).convert("RGBA"))[::-1], st.rgba)
-    # samplesPerPixel 2 on the same loop: "Samples:" counts frames x spp (Main.cu:491)
+    # samplesPerPixel 2 on the same loop: "Samples:" = (frames + 1) x spp (Main.cu:491)
     r = subprocess.run([cli, "--cpu", "--scene", "07", "--width", "64", "--height", "36", "--frames", "3",
                         "--spp", "2", "--out", str(tmp_path / "s.ppm")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    assert "Samples: 6" in r.stdout
+    assert "Samples: 8" in r.stdout
+
+
+def _denormal_07():
+    """Scene 07 with emittance and albedo scaled so the emitted radiance and
+    every accumulated frameSum value are f32 denormals."""
+    s = scenes.scene_07()
+    for i in range(s.counts[0]):
+        m = s.spheres[i].mat
+        m.emittance = m.emittance * 1e-20
+        m.albedo.x, m.albedo.y, m.albedo.z = m.albedo.x * 1e-19, m.albedo.y * 1e-19, m.albedo.z * 1e-19
+    return s
+
+
+def test_caller_ftz_daz_does_not_leak(bwrt_lib, oracle):
+    """A caller that set FTZ / DAZ on its thread (torch.set_flush_denormal, a
+    -ffast-math library) gets the same frame: the library pins the host float
+    state for its scene compile and render threads, and restores the caller's.
+    Round 3's library returned flushed frameSum values here."""
+    import torch
+    from bwrt import Renderer
+    s = _denormal_07()
+    w, h, spp, mb = 64, 36, 2, 4
+    st = oracle.render_image(s, w, h, spp, mb)
+    assert ((np.abs(st.accum) < 1.18e-38) & (st.accum != 0)).sum() > 100  # the case is live
+    with Renderer.cpu(3, lib=bwrt_lib) as c:
+        assert torch.set_flush_denormal(True)
+        try:
+            c.set_scene(s)
+            c.init_rand(w, h)
+            img = c.render(w, h, spp, mb, first_frame=1)
+            still_ftz = np.array([1e-40], dtype=np.float32) * np.float32(2)
+        finally:
+            torch.set_flush_denormal(False)
+        assert still_ftz[0] == 0.0  # the caller's FTZ / DAZ is back after the calls
+        assert np.array_equal(img, st.rgba)
+        same_state(c, st)
+
+
+def test_tuning_knobs_need_the_gate(bwrt_lib, capfd, monkeypatch):
+    """BWRT_* knobs change nothing unless BWRT_TUNING=1 (a default context
+    always takes the launch policy): BWRT_BVH_STATS's BVH report on the
+    stress scene appears only under the gate."""
+    from bwrt import Renderer
+    monkeypatch.setenv("BWRT_BVH_STATS", "1")
+    for gate, expect in (("0", False), ("1", True)):
+        monkeypatch.setenv("BWRT_TUNING", gate)
+        with Renderer.cpu(1, lib=bwrt_lib) as c:
+            c.set_scene(scenes.stress_scene())
+        err = capfd.readouterr().err
+        assert ("bvh:" in err) == expect, (gate, err)

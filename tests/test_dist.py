@@ -1,8 +1,11 @@
-"""Multi-rank path on CPU (world_size 2, gloo): the interleaved-row shard
-plan, the padded gather of RGBA8 row blocks to rank 0 and the de-interleave that
-bench.py runs over RCCL.  The per-rank renderer here is the oracle (a CPU
-stand-in for libbwrt on a GPU-less box); the GPU tests check that
-libbwrt's shards equal the full image row for row."""
+"""Multi-rank path on CPU (world_size 2 and 3, gloo): the interleaved-row
+shard plan, the padded gather of RGBA8 row blocks to rank 0 and the
+de-interleave that bench.py runs over RCCL.  Every rank renders its rows
+with the product — libbwrt.so's CPU backend (rt_create_cpu / rt_render_cpu,
+the kernels' per-ray arithmetic compiled for the host) with the rank's
+row_offset / row_stride — and the gathered frame must equal one CPU context
+rendering the whole frame and the oracle's frame; the GPU tests check that
+libbwrt's device shards equal the full image row for row."""
 import os
 import socket
 
@@ -24,17 +27,19 @@ def _free_port():
 def _worker(rank, world, port, w, h, spp, mb, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    sys.path[:0] = [os.path.join(os.path.dirname(here), "oracle"),
-                    os.path.join(os.path.dirname(here), "bwidman-raytracer_amd")]
-    import oracle as O
-    from bwrt import scenes
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "bwidman-raytracer_amd")]
+    from bwrt import Renderer, scenes
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     plan = ShardPlan(h, world, rank)
-    st = O.render_image(scenes.scene_07(), w, h, spp, mb, plan.row_offset, plan.row_stride, threads=1)
+    with Renderer.cpu(1) as c:  # the product's CPU backend, this rank's rows
+        c.set_scene(scenes.scene_07())
+        c.init_rand(w, h, plan.row_offset, plan.row_stride)
+        rgba = c.render(w, h, spp, mb, first_frame=1, row_offset=plan.row_offset, row_stride=plan.row_stride)
+    assert rgba.shape == (plan.rows, w, 4)
     block = np.zeros((plan.rows_per_shard, w), dtype=np.uint32)
-    block[:plan.rows] = st.rgba.view(np.uint32).reshape(plan.rows, w)
+    block[:plan.rows] = np.ascontiguousarray(rgba).view(np.uint32).reshape(plan.rows, w)
     gathered = gather_rows(torch.from_numpy(block.view(np.int32)).reshape(-1), plan)
     assert (gathered is None) == (rank != 0)
     if rank == 0:
@@ -57,7 +62,12 @@ def test_multi_rank_gather_matches_single_render(oracle, h, world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    from bwrt import scenes
+    from bwrt import Renderer, scenes
+    with Renderer.cpu(2) as c:  # one context, the whole frame
+        c.set_scene(scenes.scene_07())
+        c.init_rand(w, h)
+        single = c.render(w, h, spp, mb, first_frame=1)
+    assert np.array_equal(img, single)
     full = oracle.render_image(scenes.scene_07(), w, h, spp, mb).rgba
     assert np.array_equal(img, full)
 

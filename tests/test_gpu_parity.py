@@ -575,6 +575,45 @@ def test_state_writes_wait_for_device_render(gpu, oracle):
     same_state(gpu, st)
 
 
+def test_context_stream_renders_defer_their_event(gpu, oracle):
+    """Renders on the context's own stream (rt_get_stream, kernel timing off)
+    record their end event only when a later call needs it: back-to-back
+    renders on that stream, then a render on a torch stream (it must wait
+    for them), a state read and a scene upload (they must wait too), then
+    the context stream again — every frame continues the state in order."""
+    import torch
+    s = scenes.scene_07()
+    w, h, mb = 320, 180, 4
+    gpu.set_scene(s)
+    gpu.init_rand(w, h)
+    st = oracle.OracleState(w, h)
+    buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    ctx_stream = torch.cuda.ExternalStream(gpu.stream_handle())
+    other = torch.cuda.Stream()
+    gpu.set_kernel_timing(False)
+    try:
+        for f in (1, 3):  # frames 1-2, 3-4 on the context stream (handle, then NULL)
+            gpu.render_device(gpu.params(w, h, 2, mb, first_frame=f), buf.data_ptr(),
+                              ctx_stream.cuda_stream if f == 1 else None)
+        gpu.render_device(gpu.params(w, h, 2, mb, first_frame=5), buf.data_ptr(), other.cuda_stream)
+        other.synchronize()
+        oracle.render(s, st, 6, mb, first_frame=1)
+        assert np.array_equal(buf.cpu().numpy().view(np.uint8).reshape(h, w, 4), st.rgba)
+        same_state(gpu, st)
+        gpu.render_device(gpu.params(w, h, 2, mb, first_frame=7), buf.data_ptr(), None)
+        rng, _ = gpu.get_state(h, w)  # waits for the deferred event's render
+        oracle.render(s, st, 2, mb, first_frame=7)
+        assert np.array_equal(rng, st.rng)
+        gpu.render_device(gpu.params(w, h, 2, mb, first_frame=9), buf.data_ptr(), None)
+        gpu.set_scene(scenes.scene_04())  # must not swap the scene under the running render
+        ctx_stream.synchronize()
+        oracle.render(s, st, 2, mb, first_frame=9)
+        assert np.array_equal(buf.cpu().numpy().view(np.uint8).reshape(h, w, 4), st.rgba)
+    finally:
+        gpu.set_kernel_timing(True)
+        gpu.set_scene(s)
+
+
 def test_cli_progressive_loop_with_controls(bwrt_lib, oracle, tmp_path):
     """The C++ host loop (host/bwrt_render.cpp, Main.cu:467-496): 2 frames,
     then W+LEFT held for one frame (controls() restarts accumulation), then 4
@@ -601,7 +640,8 @@ def test_cli_progressive_loop_with_controls(bwrt_lib, oracle, tmp_path):
     oracle.render(s2, st, 4, 5, first_frame=1)
     img = np.asarray(Image.open(png).convert("RGBA"))[::-1]
     assert np.array_equal(img, st.rgba)
-    assert "camera" in r.stdout and "Samples: 4" in r.stdout
+    # 4 frames since the reset by the move: accumulatedFrames = 5 (Main.cu:480-491)
+    assert "camera" in r.stdout and "Samples: 5" in r.stdout
     # the same loop across 3 contexts (rt_render_multi; one device here)
     png3 = tmp_path / "out3.png"
     r = subprocess.run([cli, "--scene", "07", "--width", "160", "--height", "90", "--frames", "6", "--gpus", "3",
@@ -721,6 +761,28 @@ def test_global_records_forced(bwrt_lib, oracle, monkeypatch, block, w, h, mb):
         r.close()
 
 
+@pytest.mark.parametrize("block", [64, 128, 256])
+@pytest.mark.parametrize("tail", [0, 1, 5, 16])
+@pytest.mark.parametrize("grec", [0, 1])
+def test_tail_mode_forced(bwrt_lib, oracle, monkeypatch, block, tail, grec):
+    """The sorted kernel's tail mode (a group's last <= BWRT_TAIL live pixels
+    finished by its first wave, several lanes per pixel splitting each closest
+    hit) at every workgroup size and with LDS / global records: the 07 scene
+    (shared pyramid edges: exact ties between triangles), the quad box, a
+    seeded random scene, and one scaled by 1e10 (rays whose tests could
+    overflow take the serial loop inside the tail).  tail 0 = off."""
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_TAIL=tail, BWRT_BLOCK=block, BWRT_GREC=grec)
+    cases = [(scenes.scene_07(), 160, 90, 3, 4, 0, 1), (scenes.scene_04_box(), 96, 61, 2, 5, 1, 3),
+             (_random_scene(7), 80, 45, 2, 6, 0, 1), (_scaled(_random_scene(3), 1e10), 64, 36, 2, 5, 0, 1)]
+    try:
+        for scene, w, h, spp, mb, off, stride in cases:
+            img, st = run_pair(r, oracle, scene, w, h, spp, mb, row_offset=off, row_stride=stride)
+            assert np.array_equal(img, st.rgba)
+            same_state(r, st)
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("name", ["07", "04_box"])
 def test_simple_kernel_ab_reference(bwrt_lib, oracle, monkeypatch, name):
     """The one-path-per-lane kernel kept as the A/B reference (BWRT_KERNEL=simple)."""
@@ -755,8 +817,9 @@ def test_launch_order_feedback_bvh_refill(bwrt_lib, monkeypatch):
     """Launch-order feedback in the BVH ray-refill kernel (config 5's
     product path): the stress scene at 1920x1080, 2 spp, 8 bounces — a grid
     of 32,400 single-wave groups, several resident generations — rendered
-    four times (blockIdx order, then in orders re-sorted every 2nd launch)
-    and once as a continuation; every image, frameSum and RNG state
+    four times (blockIdx order, then reordered: BVH scenes re-sort their
+    order after every launch, so kept orders are covered by
+    test_launch_order_feedback only) and once as a continuation; every image, frameSum and RNG state
     equals the product's CPU fallback (itself pinned to the oracle,
     tests/test_cpu_fallback.py; the brute-force oracle would need minutes)."""
     from bwrt import Renderer
@@ -768,7 +831,7 @@ def test_launch_order_feedback_bvh_refill(bwrt_lib, monkeypatch):
         want_rng, _ = c.get_state(1080, 1920)
         cont = c.render(1920, 1080, 1, 8, want_accum=True)
         cont_rng, _ = c.get_state(1080, 1920)
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1, BWRT_ORDER_PERIOD=2)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_ORDER=1)
     try:
         r.set_scene(s)
         for _ in range(4):

@@ -2,6 +2,7 @@
 # c3 A/B of a variant library (tools/variants.sh NAME): the config-3 parity
 # subset, then alternating full-frame benches and shard sweeps.
 # usage: CAND=name [ROUNDS=3] [STRIDES=1,4,8] bash tools/ab_c3.sh
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 V=$PWD/bwidman-raytracer_amd/build/variants
 mkdir -p gpurun_out/ab_c3

@@ -2,6 +2,7 @@
 # c5 (BVH refill kernel) A/B on the GPU box: the BVH / stress parity subset
 # with each candidate library, then alternating c5 bench runs over leaf-batch
 # thresholds.  usage: LIBS="base park1" BATCHES="60 48" ROUNDS=2 bash tools/ab_c5.sh
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 V=$PWD/bwidman-raytracer_amd/build/variants
 mkdir -p gpurun_out/ab_c5

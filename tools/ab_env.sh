@@ -2,6 +2,7 @@
 # A/B of (variant library, environment) pairs on the GPU box, alternating
 # bench runs.  usage: ROUNDS=3 CONFIG=c3 bash tools/ab_env.sh "label:variant:ENV=1,ENV2=2" ...
 # (variant "base" = lib/libbwrt.so; env list may be empty)
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 V=$PWD/bwidman-raytracer_amd/build/variants
 mkdir -p gpurun_out/ab_env

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B timing of built variants on the GPU box: tools/ab_libs.sh ROUNDS name... ("base" = lib/libbwrt.so)
 # extra bench args via BENCH_ARGS
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 V=$PWD/bwidman-raytracer_amd/build/variants
 R=$1; shift
 for r in $(seq $R); do

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of launch-order feedback variants on c3 row shards: tools/ab_order.sh name... ("base" = lib/libbwrt.so)
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 for v in "$@"; do
   L=$PWD/bwidman-raytracer_amd/build/variants/$v/libbwrt.so; [ $v = base ] && L=$PWD/bwidman-raytracer_amd/lib/libbwrt.so

@@ -1,6 +1,7 @@
 #!/bin/bash
 # c5 launch-order feedback A/B (refill kernel): parity subset, then alternating
 # c5 benches with BWRT_ORDER=0 / 1.  usage: bash tools/ab_order_c5.sh
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 mkdir -p gpurun_out/ord
 timeout -k 10 400 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread \

@@ -4,6 +4,7 @@
 # usage: A=label:path B=label:path [ROUNDS=3] [CONFIGS="c3 c4"] [STRIDES=1,4,8,16] bash tools/ab_pair.sh
 # (path "base" = bwidman-raytracer_amd/lib/libbwrt.so, otherwise a variant name
 # under bwidman-raytracer_amd/build/variants)
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 V=$PWD/bwidman-raytracer_amd/build/variants
 OUT=gpurun_out/ab_pair; mkdir -p $OUT

@@ -4,6 +4,7 @@
 # candidate library, then 5 alternating c3 and 2 c4 bench runs.
 # usage: CAND=name [BASE=name] [SUBSET=expr] bash tools/ab_run.sh
 # (variants from tools/variants.sh; BASE=base is lib/libbwrt.so)
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 V=$PWD/bwidman-raytracer_amd/build/variants
 CAND=${CAND:?set CAND to a tools/variants.sh name}; BASE=${BASE:-base}

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of built variants on one row shard: tools/ab_shard.sh CONFIG STRIDE name... ("base" = lib/libbwrt.so)
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 C=$1; S=$2; shift 2
 for v in "$@"; do
   L=$PWD/bwidman-raytracer_amd/build/variants/$v/libbwrt.so; [ $v = base ] && L=$PWD/bwidman-raytracer_amd/lib/libbwrt.so

@@ -2,6 +2,7 @@
 # Rehearse bench.py's N > 1 path on one GPU box: 2 and 3 ranks sharing the GPU over
 # gloo (staged through the host), with and without frame pipelining, --verify
 # checks the gathered frame against a 1-GPU render.  Then a shard sweep and the N=1 bench.
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
 mkdir -p gpurun_out
 for n in 2 3; do

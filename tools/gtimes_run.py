@@ -3,6 +3,8 @@
 group-duration spread and the chip's active-group count over time.
 usage: BWRT_LIB=.../gtimes/libbwrt.so tools/gtimes_run.py [config] [stride]"""
 import os
+
+os.environ.setdefault("BWRT_TUNING", "1")  # the library reads BWRT_* knobs only under it
 import sys
 
 import numpy as np

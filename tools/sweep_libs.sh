@@ -1,6 +1,7 @@
 #!/bin/bash
 # Shard-sweep kernel times for several built variants on the GPU box:
 # tools/sweep_libs.sh "STRIDES" name... ("base" = lib/libbwrt.so); extra args via SWEEP_ARGS
+export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 V=$PWD/bwidman-raytracer_amd/build/variants
 S=$1; shift
 for v in "$@"; do
