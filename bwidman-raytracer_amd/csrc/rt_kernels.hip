@@ -641,9 +641,54 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 
 
 
-// Tail mode of rt_render_sorted_kernel (see there): wave 0 finishes the
-// group's last `live` pixels from their hand-off records H; segments of S
-// lanes per pixel run its tasks redundantly and split its closest hits
+// specular_scatter (rt_path.h, Main.cu:245-255) for a tail segment whose
+// lanes hold the same ray: the two sincos_nn of the microfacet sample and the
+// two G1 terms of specularWeight each run on partner lanes (sl even / odd,
+// exchanged with a DPP quad_perm [1,0,3,2]), so a lone path's SPEC task
+// carries one of each on its dependency chain.  Same operations, same
+// operands, same results (a float product is commutative).  Needs S >= 2.
+__device__ __forceinline__ f3 specular_scatter_pair(Xorwow& rs, f3 d, f3 n, float rough, float rough2, float ior2m1,
+                                                    float& kspec, int sl) {
+    const bool odd = sl & 1;
+    const float e1 = rand_range(rs, 1.0f);
+    const float e2 = rand_range(rs, 1.0f);
+    const float theta = atan_nn(rough * rt_sqrt(e1) / rt_sqrt(1.0f - e1));
+    const float phi = 2.0f * RT_PI * e2;
+    float s_, c_;
+    sincos_nn(odd ? phi : theta, s_, c_);
+    const float s2 = __int_as_float(dpp_i<0xB1>(__float_as_int(s_)));
+    const float c2 = __int_as_float(dpp_i<0xB1>(__float_as_int(c_)));
+    const float st = odd ? s2 : s_, ct = odd ? c2 : c_;  // theta's, from the even lane
+    const float sp = odd ? s_ : s2, cp = odd ? c_ : c2;  // phi's, from the odd lane
+    const f3 mloc = mk(st * cp, st * sp, ct);
+    f3 some = mk(1.0f, 0.0f, 0.0f);
+    if (fabsf(dot(n, some)) < 1.0f - RT_NEAR_ZERO) some = mk(0.0f, 1.0f, 0.0f);
+    const f3 t1 = cross(n, some);
+    const f3 t2 = cross(n, t1);
+    const f3 m = mk(dot(mk(t1.x, t2.x, n.x), mloc), dot(mk(t1.y, t2.y, n.y), mloc), dot(mk(t1.z, t2.z, n.z), mloc));
+    const f3 scatter = sub(d, scale(2.0f * dot(d, m), m));
+    const f3 inc = scale(-1.0f, d);
+    const float fr = fresnel(inc, m, ior2m1);
+    // specular_weight(inc, scatter, n, m, rough2): G1(inc) on the even lane,
+    // G1(scatter) on the odd one
+    const float g1 = shadowing_masking(odd ? scatter : inc, n, m, rough2);
+    const float g1p = __int_as_float(dpp_i<0xB1>(__float_as_int(g1)));
+    float g = g1 * g1p;
+    float sw;
+    if (isnan(g)) {
+        sw = 1.0f;
+    } else {
+        float den = fabsf(dot(inc, n) * dot(m, n));
+        if (den == 0.0f) den = RT_NEAR_ZERO;
+        sw = fabsf(dot(inc, m)) * g / den;
+    }
+    kspec = sw * fr / RT_SPECULAR_CHANCE;
+    return scatter;
+}
+
+// Tail mode of rt_render_sorted_kernel (see there): a wave finishes its own
+// last `live` pixels from their hand-off records H; segments of S lanes per
+// pixel run its tasks redundantly and split its closest hits
 // (coop_closest_hit).  Not inlined (see the call).
 enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };  // a lane's next task
 template <int BLOCK, bool HIT_LDS, bool GREC, bool QUADS>
@@ -662,15 +707,16 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
     const __attribute__((address_space(4))) rt_kparams* kp =
         (const __attribute__((address_space(4))) rt_kparams*)(((unsigned long long)kp_hi << 32) | kp_lo);
     const rt_kparams& K = *(const rt_kparams*)kp;
-    const int tail_live = __builtin_amdgcn_readfirstlane(tail_live_arg);
-    const int tid = threadIdx.x;
+    const int tail_live = __builtin_amdgcn_readfirstlane(tail_live_arg);  // this wave's live pixels
+    const int tid = threadIdx.x & 63;
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const float* hit_tab = HIT_LDS ? smem : K.hit;
     float* rec_base = HIT_LDS ? smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3) : smem;
     const int levels = K.max_bounces;
     const int LL = GREC ? (levels < RT_GREC_LDS_LEVELS ? levels : RT_GREC_LDS_LEVELS) : levels;
-    const lds_float* H = (const lds_float*)(rec_base + 3 * LL * BLOCK);
-    const lds_float* sc = H + RT_TAIL_FIELDS * RT_TAIL_MAX;
+    const lds_float* slots = (const lds_float*)(rec_base + 3 * LL * BLOCK);
+    const lds_float* H = slots + (threadIdx.x >> 6) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
+    const lds_float* sc = slots + (BLOCK / 64) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
     const long npix = (long)K.rows * K.width;
     const int GL = K.max_bounces - LL;
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
@@ -736,7 +782,7 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
                 int code = thid;
                 if (tmode == T_SPEC) {  // Main.cu:245-255
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * thid + 8);
-                    td = specular_scatter(q.rs, td, thn, h2.x, h2.z, h2.y, kspec);
+                    td = specular_scatter_pair(q.rs, td, thn, h2.x, h2.z, h2.y, kspec, sl);  // S >= 4 here
                     code = ~thid;
                 } else {  // diffuse, Main.cu:257-260
                     td = random_direction(q.rs, thn);
@@ -1036,11 +1082,10 @@ rt_render_sorted_kernel(rt_kparams K) {
         const int nf = cnt[0], nb = cnt[1];
         if (nf + nb == 0) break;
 #if RT_TAIL
-        // few live pixels left (one per posted task; group-uniform): hand
-        // them to wave 0's tail loop below instead of running this round
+        // few live pixels left (one per posted task; group-uniform): each
+        // wave finishes its own in the tail loop below instead of this round
         if (!BVH && nf + nb <= K.tail_n) {
             tail_live = nf + nb;
-            tail_c = slot < 0 ? -1 : slot < nf ? slot : nf + (BLOCK - 1 - slot);
             break;
         }
 #endif
@@ -1230,15 +1275,19 @@ rt_render_sorted_kernel(rt_kparams K) {
 #if RT_TAIL
     if (!BVH && tail_live > 0) {  // group-uniform
         // ---- tail mode.  The group's few live pixels (each with its task of
-        // this round still to run) move to wave 0, which finishes them in a
-        // loop of its own: no barriers, no task slots, and each pixel held
+        // this round still to run) leave the round loop: every wave finishes
+        // its own in a loop without barriers or task slots, each pixel held
         // by a segment of S lanes that run its tasks redundantly (the same
         // RNG stream, the same results) and split its closest hits.  The
-        // other waves leave.  Hand-off record [field][pixel] in the task-slot
-        // area (free: this round's slots are never executed), the scene's
-        // records behind it (the launcher checks that both fit).
-        lds_float* H = (lds_float*)slots;
-        lds_float* sc = H + RT_TAIL_FIELDS * RT_TAIL_MAX;
+        // hand-off records [field][pixel] go to the task-slot area (free:
+        // this round's slots are never executed), one per wave, the scene's
+        // records behind them (the launcher checks that all fit).
+        // every wave keeps its own live pixels: wave w's hand-off record at
+        // slots + w * RT_TAIL_FIELDS * RT_TAIL_MAX, index = live lanes below
+        const unsigned long long live_mask = __ballot(mode != T_NONE);
+        if (mode != T_NONE) tail_c = lanes_below(live_mask);
+        lds_float* H = (lds_float*)slots + (tid >> 6) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
+        lds_float* sc = (lds_float*)slots + (BLOCK / 64) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
         if (tail_c >= 0) {
 #define HW(f, v) H[(f) * RT_TAIL_MAX + tail_c] = (v)
             HW(0, __int_as_float((int)px.p));
@@ -1275,13 +1324,15 @@ rt_render_sorted_kernel(rt_kparams K) {
                         (QUADS ? RT_QUAD_FLOATS * K.n_quad : 0);
         for (int i = tid; i < nsc; i += BLOCK) sc[i] = K.sph[i];  // sph | pln | tri | quad are contiguous
         __syncthreads();
-        if (tid < 64) {
+        if (live_mask) {  // (wave-uniform)
             // a call, not inlined: the tail's registers stay out of the main
             // loop's allocation (inlined, it cost the global-record kernel 6
             // spilled VGPRs and 29 more spilled SGPRs)
             rt_tail_run<BLOCK, HIT_LDS, GREC, QUADS>(
-                (const __attribute__((address_space(4))) rt_kparams*)__builtin_amdgcn_kernarg_segment_ptr(), tail_live);
+                (const __attribute__((address_space(4))) rt_kparams*)__builtin_amdgcn_kernarg_segment_ptr(),
+                __popcll(live_mask));
         }
+        __syncthreads();  // the group's span (ORDER, GTIMES) ends with its last wave
     }
 #endif
     // the loop exit is group-uniform (the round that posts no task), so one
@@ -1628,7 +1679,8 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     if (K.tail_n > 0) {
         const long nsc = (long)RT_SPH_FLOATS * K.n_sph + (long)RT_PLN_FLOATS * K.n_pln +
                          (long)RT_TRI_FLOATS * K.n_tri + (long)RT_QUAD_FLOATS * K.n_quad;
-        if (!SORTED || BVH || !RT_TAIL || (long)RT_TAIL_FIELDS * RT_TAIL_MAX + nsc > 13L * BLOCK) K.tail_n = 0;
+        if (!SORTED || BVH || !RT_TAIL || (long)(BLOCK / 64) * RT_TAIL_FIELDS * RT_TAIL_MAX + nsc > 13L * BLOCK)
+            K.tail_n = 0;
         if (K.tail_n > RT_TAIL_MAX) K.tail_n = RT_TAIL_MAX;
     }
     // launch-order feedback: only where the sorted grid covers every item

@@ -33,6 +33,17 @@
  *    frameSum/n -> ACES -> gamma -> *255 -> round -> u8.
  *  - The per-pixel RNG is cuRAND-XORWOW seeded with the global pixel index
  *    y*width+x (Main.cu:377); results are independent of sharding.
+ *  - Launch-policy overrides for tuning and diagnostics are environment
+ *    variables read ONLY when the process sets BWRT_TUNING=1 (otherwise a
+ *    context always takes the measured launch policy); none changes a
+ *    result, only kernel choice and speed:
+ *      at rt_create:    BWRT_KERNEL=simple, BWRT_BLOCK, BWRT_TILE, BWRT_TILE_SQ,
+ *                       BWRT_GREC, BWRT_GRID_MULT, BWRT_LEAF_BATCH, BWRT_REFILL,
+ *                       BWRT_TAIL, BWRT_BVH_REFILL, BWRT_ORDER, BWRT_ORDER_PERIOD
+ *      at rt_set_scene: BWRT_BVH_MIN, BWRT_BVH_LEAF, BWRT_BVH_CT, BWRT_BVH_SBVH,
+ *                       BWRT_BVH_REFS, BWRT_BVH_ALPHA, BWRT_BVH_ORDER_MASK,
+ *                       BWRT_BVH_N16, BWRT_NO_CULL, BWRT_BVH_STATS (report)
+ *      per launch:      BWRT_STAMPS, BWRT_GTIMES (diagnostic builds only)
  */
 #ifndef RT_ABI_H
 #define RT_ABI_H
