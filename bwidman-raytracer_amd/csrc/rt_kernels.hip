@@ -723,7 +723,10 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
     const f3 o = mk(0.0f, 0.0f, 0.0f), d = o, hn = o;
     // segment size: 64 / (live pixels rounded up to a power of 2), at most 16
     const int p2 = tail_live <= 1 ? 1 : 1 << (32 - __builtin_clz(tail_live - 1));
-    const int S = 64 / p2 < 16 ? 64 / p2 : 16;
+#ifndef RT_TAIL_COOP  // A/B builds: 0 = one lane per pixel (the barrier-free loop alone)
+#define RT_TAIL_COOP 1
+#endif
+    const int S = !RT_TAIL_COOP ? 1 : 64 / p2 < 16 ? 64 / p2 : 16;
     const int seg = tid / S, sl = tid - seg * S;
     bool live = seg < tail_live;
     PixelState q;
@@ -782,7 +785,10 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
                 int code = thid;
                 if (tmode == T_SPEC) {  // Main.cu:245-255
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * thid + 8);
-                    td = specular_scatter_pair(q.rs, td, thn, h2.x, h2.z, h2.y, kspec, sl);  // S >= 4 here
+                    if (RT_TAIL_COOP)
+                        td = specular_scatter_pair(q.rs, td, thn, h2.x, h2.z, h2.y, kspec, sl);  // S >= 4 here
+                    else
+                        td = specular_scatter(q.rs, td, thn, h2.x, h2.z, h2.y, kspec);
                     code = ~thid;
                 } else {  // diffuse, Main.cu:257-260
                     td = random_direction(q.rs, thn);
@@ -814,7 +820,7 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
         float t = INFINITY;
         int id = -1;
         if (has_ray) {
-            if (bvh_safe(K, to, td))
+            if (RT_TAIL_COOP && bvh_safe(K, to, td))
                 coop_closest_hit<QUADS>(K, sc, to, td, sl, S, t, id);
             else  // NaN-capable tests: the reference's own loop order
                 closest_hit_brute<QUADS>(K, to, td, t, id);

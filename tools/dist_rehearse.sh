@@ -7,8 +7,9 @@ set -o pipefail
 mkdir -p gpurun_out
 for n in 2 3; do
   for ov in "" "--no-overlap"; do
-    BWRT_DIST_BACKEND=gloo timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus $n --steps 10 --warmup 3 --verify $ov > gpurun_out/dist_$n$ov.log 2>&1 || { echo "FAIL $n $ov"; tail -20 gpurun_out/dist_$n$ov.log; exit 1; }
-    echo "n=$n $ov: $(grep -o '"ms_per_step[^,]*' gpurun_out/dist_$n$ov.log) $(grep verify gpurun_out/dist_$n$ov.log)"
+    BWRT_DIST_BACKEND=gloo timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus $n --steps 10 --warmup 3 $ov > gpurun_out/dist_$n$ov.log 2>&1 || { echo "FAIL $n $ov"; tail -20 gpurun_out/dist_$n$ov.log; exit 1; }
+    echo "n=$n $ov: $(grep -o '"ms_per_step[^,]*' gpurun_out/dist_$n$ov.log) $(grep -o '"verified[^,]*' gpurun_out/dist_$n$ov.log) $(grep -o '"kernel_ms_avg[^,]*' gpurun_out/dist_$n$ov.log)"
+    grep -q '"verified": true' gpurun_out/dist_$n$ov.log || { echo "not verified"; exit 1; }
   done
 done
 timeout -k 10 100 python -u tools/shard_sweep.py --blocks 0 --strides 1,2,4,8 2>&1 | grep -v amdgpu.ids
