@@ -934,6 +934,10 @@ rt_render_sorted_kernel(rt_kparams K) {
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
     if (tid < 4) counters[tid] = 0;
+    // counters[4]: the tail threshold, read with the queue counters each
+    // round (from the kernel arguments it is an extra scalar load and wait
+    // per round: the loop's SGPRs do not keep it)
+    if (tid == 4) counters[4] = K.tail_n;
 #ifdef RT_GTIMES
     // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g], [2g+1]
     if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1086,11 +1090,15 @@ rt_render_sorted_kernel(rt_kparams K) {
         // no task anywhere in the workgroup: every lane is idle (rays are
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
+#if RT_TAIL
+        const int tail_thr = counters[4];
+        asm volatile("" ::"v"(tail_thr));  // read together with the counters (one LDS wait)
+#endif
         if (nf + nb == 0) break;
 #if RT_TAIL
         // few live pixels left (one per posted task; group-uniform): each
         // wave finishes its own in the tail loop below instead of this round
-        if (!BVH && nf + nb <= K.tail_n) {
+        if (!BVH && nf + nb <= tail_thr) {
             tail_live = nf + nb;
             break;
         }
@@ -1873,7 +1881,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int lds_levels = sorted && K.rec ? (K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS)
                                            : K.max_bounces + (sorted ? 0 : 1);
     size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * block * sizeof(float);
-    if (sorted) b += (size_t)13 * block * sizeof(float) + 4 * sizeof(int);
+    if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);  // + counters, tail threshold
     return b;
 }
 
