@@ -382,6 +382,14 @@ __device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_
 #ifndef RT_TAIL
 #define RT_TAIL 1
 #endif
+// deferred fold (global-record kernels): a finished path's records are
+// folded by the executor of the pixel's next front task (its camera ray, or
+// a fold-only task after its last frame) instead of by the owner lane in the
+// I-phase, where only the lanes whose path just ended run it (9.3 of 64
+// lanes per instruction, profiles/r04/check_a/phase_lanes.json)
+#ifndef RT_DEFER_FOLD
+#define RT_DEFER_FOLD 1
+#endif
 
 template <int BLOCK, bool HIT_LDS, bool BVH>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
@@ -691,6 +699,9 @@ __device__ __forceinline__ f3 specular_scatter_pair(Xorwow& rs, f3 d, f3 n, floa
 // pixel run its tasks redundantly and split its closest hits
 // (coop_closest_hit).  Not inlined (see the call).
 enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };  // a lane's next task
+// deferred fold (RT_DEFER_FOLD): the lane's finished path waits to be folded
+// by its next front task (T_REGEN | T_FOLD, or T_FOLD alone after the last frame)
+enum { T_FOLD = 8 };
 template <int BLOCK, bool HIT_LDS, bool GREC, bool QUADS>
 __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((address_space(4))) rt_kparams* kp_arg,
                                                       int tail_live_arg) {
@@ -758,7 +769,40 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
 #undef HR
     }
     lds_float* trec = (lds_float*)(rec_base + otid);
-    float* tgrec = GREC ? K.rec + (long)blockIdx.x * 3 * GL * BLOCK + otid : rec_base;
+    constexpr bool DF = GREC && RT_DEFER_FOLD;  // (the kernel's deferred fold: its record layout)
+    const int GLD = DF ? GL + 1 : GL;
+    float* tgrec = GREC ? K.rec + (long)blockIdx.x * 3 * GLD * BLOCK + otid : rec_base;
+    if (DF && live && (tmode & T_FOLD)) {  // a finished path handed over unfolded
+        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];
+        if (tdepth > K.max_bounces) {
+            const float* r = tgrec + 3 * GL * BLOCK;
+            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+        }
+        const int nrec = tdepth > K.max_bounces ? K.max_bounces : tdepth;
+        for (int l = nrec - 1; l >= LL; --l) {
+            const float* r = tgrec + 3 * (l - LL) * BLOCK;
+            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+        }
+        for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
+            const lds_float* r = trec + 3 * l * BLOCK;
+            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+        }
+        if (q.frame == 1u) {
+            q.ax = 0.0f;
+            q.ay = 0.0f;
+            q.az = 0.0f;
+        }
+        q.ax = q.ax + lx;
+        q.ay = q.ay + ly;
+        q.az = q.az + lz;
+        q.frame++;
+        q.passes_left--;
+        tmode &= 7;  // T_REGEN, or T_NONE after the last frame
+        if (tmode == T_NONE) {
+            store_pixel(K, npix, q);
+            live = false;
+        }
+    }
 #ifdef RT_STAMPS
     // diagnostic: K.stamps[32] tail wave-cycles, [33] tail rounds, [34]
     // tail entries, [35] pixels handed over
@@ -898,8 +942,10 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
 //
 // LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
-template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(!BVH && (GREC || RT_TAIL) ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
+// TAIL: the tail-mode instantiation (launched only when K.tail_n > 0: its
+// code costs the main loop spilled SGPRs even when no group enters it)
+template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true, bool TAIL = false>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(!BVH && (GREC || TAIL) ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
@@ -927,7 +973,11 @@ rt_render_sorted_kernel(rt_kparams K) {
     // base held across the loop)
     lds_float* rec = (lds_float*)(rec_base + tid);
     const int GL = levels - LL;
-    float* grec = GREC ? K.rec + (long)blockIdx.x * 3 * GL * BLOCK + tid : rec_base;
+    // deferred fold: the deepest level (max_bounces) goes to global memory
+    // too, as level GL, so it outlives the round that made it
+    constexpr bool DF = GREC && !BVH && RT_DEFER_FOLD;
+    const int GLD = DF ? GL + 1 : GL;
+    float* grec = GREC ? K.rec + (long)blockIdx.x * 3 * GLD * BLOCK + tid : rec_base;
     float* slots = rec_base + 3 * LL * BLOCK;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
     // counters[0..3]: queue fronts/backs (2 parities)
@@ -937,7 +987,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     // counters[4]: the tail threshold, read with the queue counters each
     // round (from the kernel arguments it is an extra scalar load and wait
     // per round: the loop's SGPRs do not keep it)
-    if (tid == 4) counters[4] = K.tail_n;
+    if (TAIL && tid == 4) counters[4] = K.tail_n;
 #ifdef RT_GTIMES
     // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g], [2g+1]
     if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1055,7 +1105,8 @@ rt_render_sorted_kernel(rt_kparams K) {
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
         int* cnt = counters + 2 * parity;
-        const bool front = task == T_REGEN || task == T_DIFF;
+        // (deferred fold: T_REGEN | T_FOLD and T_FOLD alone are front tasks)
+        const bool front = DF ? ((task & 7) == T_REGEN || task == T_DIFF || task == T_FOLD) : task == T_REGEN || task == T_DIFF;
         const unsigned long long mf = __ballot(front);
         const unsigned long long mbk = __ballot(task == T_SPEC);
         int base_f = 0, base_b = 0;
@@ -1069,14 +1120,18 @@ rt_render_sorted_kernel(rt_kparams K) {
         if (front) slot = base_f + lanes_below(mf);
         if (task == T_SPEC) slot = BLOCK - 1 - (base_b + lanes_below(mbk));
         if (slot >= 0) {
-            const f3 nrm = task == T_REGEN ? px.d0 : hn;
+            const f3 nrm = (DF ? (task & 7) == T_REGEN : task == T_REGEN) ? px.d0 : hn;
             SLOT(0, slot) = nrm.x;
             SLOT(1, slot) = nrm.y;
             SLOT(2, slot) = nrm.z;
             SLOT(3, slot) = d.x;
             SLOT(4, slot) = d.y;
             SLOT(5, slot) = d.z;
-            SLOT(6, slot) = __int_as_float(task == T_REGEN ? -1 : hid);
+            // code: primitive id (bounce), -1 (camera ray), or for a deferred
+            // fold -(2 + depth + 64 tid [+ 2^20 when no camera ray follows])
+            int code = task == T_REGEN ? -1 : hid;
+            if (DF && (task & T_FOLD)) code = -(2 + depth + 64 * tid + (task == T_FOLD ? (1 << 20) : 0));
+            SLOT(6, slot) = __int_as_float(code);
             SLOT(7, slot) = __uint_as_float(px.rs.d);
             SLOT(8, slot) = __uint_as_float(px.rs.v0);
             SLOT(9, slot) = __uint_as_float(px.rs.v1);
@@ -1090,19 +1145,18 @@ rt_render_sorted_kernel(rt_kparams K) {
         // no task anywhere in the workgroup: every lane is idle (rays are
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
-#if RT_TAIL
-        const int tail_thr = counters[4];
-        asm volatile("" ::"v"(tail_thr));  // read together with the counters (one LDS wait)
-#endif
+        int tail_thr = 0;
+        if (TAIL) {
+            tail_thr = counters[4];
+            asm volatile("" ::"v"(tail_thr));  // read together with the counters (one LDS wait)
+        }
         if (nf + nb == 0) break;
-#if RT_TAIL
         // few live pixels left (one per posted task; group-uniform): each
         // wave finishes its own in the tail loop below instead of this round
-        if (!BVH && nf + nb <= tail_thr) {
+        if (TAIL && !BVH && nf + nb <= tail_thr) {
             tail_live = nf + nb;
             break;
         }
-#endif
 
         // ---- T-phase: execute slot `tid`
         {
@@ -1142,8 +1196,38 @@ rt_render_sorted_kernel(rt_kparams K) {
                         keep_i((int)r2.v4);
                     }
 #endif
-                    r = random_direction(rs, nrm, rej_ptr);
-                    if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
+                    const bool fold = DF && code < -1;  // a finished path to fold
+                    const int fv = -code - 2;           // (fold) depth | tid << 6 | fold-only << 20
+                    r = nrm;
+                    if (!fold || !(fv >> 20)) {
+                        r = random_direction(rs, nrm, rej_ptr);
+                        if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
+                    }
+                    if (fold) {
+                        // the owner's finished path, innermost-first (Main.cu:262-268),
+                        // from its record stack: level max_bounces and the deep
+                        // levels in global memory, the shallow ones in LDS
+                        const int od = fv & 63, ot = (fv >> 6) & 1023;
+                        const float* gq = K.rec + (long)blockIdx.x * 3 * GLD * BLOCK + ot;
+                        const lds_float* lq = (const lds_float*)(rec_base + ot);
+                        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
+                        if (od > K.max_bounces) {
+                            const float* q = gq + 3 * GL * BLOCK;
+                            fold_level(__float_as_int(q[0]), q[BLOCK], q[2 * BLOCK], hit_tab, lx, ly, lz);
+                        }
+                        const int nrec = od > K.max_bounces ? K.max_bounces : od;
+                        for (int l = nrec - 1; l >= LL; --l) {
+                            const float* q = gq + 3 * (l - LL) * BLOCK;
+                            fold_level(__float_as_int(q[0]), q[BLOCK], q[2 * BLOCK], hit_tab, lx, ly, lz);
+                        }
+                        for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
+                            const lds_float* q = lq + 3 * l * BLOCK;
+                            fold_level(__float_as_int(q[0]), q[BLOCK], q[2 * BLOCK], hit_tab, lx, ly, lz);
+                        }
+                        SLOT(4, tid) = lx;  // (slot fields 4..6 are free once read)
+                        SLOT(5, tid) = ly;
+                        SLOT(6, tid) = lz;
+                    }
                 } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
@@ -1211,10 +1295,25 @@ rt_render_sorted_kernel(rt_kparams K) {
             px.rs.v3 = __float_as_uint(RES(8, slot));
             px.rs.v4 = __float_as_uint(RES(9, slot));
             mode = T_NONE;
-            if (task == T_REGEN) {
-                o = cam;
-                depth = 0;
-                has_ray = true;
+            if (DF ? (task & 7) == T_REGEN || task == T_FOLD : task == T_REGEN) {
+                if (DF && (task & T_FOLD)) {  // the finished path, folded by the executor
+                    const float lx = SLOT(4, slot), ly = SLOT(5, slot), lz = SLOT(6, slot);
+                    if (px.frame == 1u) {  // progressive accumulation (Main.cu:299-304)
+                        px.ax = 0.0f;
+                        px.ay = 0.0f;
+                        px.az = 0.0f;
+                    }
+                    px.ax = px.ax + lx;
+                    px.ay = px.ay + ly;
+                    px.az = px.az + lz;
+                    px.frame++;
+                    px.passes_left--;
+                }
+                if (task != T_FOLD) {
+                    o = cam;
+                    depth = 0;
+                    has_ray = true;
+                }
             } else {
                 const int code = task == T_SPEC ? ~hid : hid;
                 const float kspec = task == T_SPEC ? RES(3, slot) : 0.0f;
@@ -1233,9 +1332,16 @@ rt_render_sorted_kernel(rt_kparams K) {
                     }
                     has_ray = true;  // from the hit point o along d
                 } else {  // next query would exceed maxBounces (Main.cu:210): the path ends
-                    SLOT(4, slot) = kspec;
-                    SLOT(5, slot) = cosang;
-                    SLOT(6, slot) = __int_as_float(code);
+                    if (DF) {  // the deepest level: global level GL, folded next round
+                        float* r = grec + 3 * GL * BLOCK;
+                        r[0] = __int_as_float(code);
+                        r[BLOCK] = kspec;
+                        r[2 * BLOCK] = cosang;
+                    } else {
+                        SLOT(4, slot) = kspec;
+                        SLOT(5, slot) = cosang;
+                        SLOT(6, slot) = __int_as_float(code);
+                    }
                     ended = true;
                 }
                 depth++;
@@ -1281,13 +1387,16 @@ rt_render_sorted_kernel(rt_kparams K) {
         }
         if (ended) {
             ended = false;
-            finish_path(slot);
+            if (DF)  // folded by the pixel's next front task: its camera ray, or a fold-only task
+                mode = (px.passes_left > 1 ? T_REGEN : T_NONE) | T_FOLD;
+            else
+                finish_path(slot);
         }
         STAMP(6);
     }
     if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
 #if RT_TAIL
-    if (!BVH && tail_live > 0) {  // group-uniform
+    if (TAIL && !BVH && tail_live > 0) {  // group-uniform
         // ---- tail mode.  The group's few live pixels (each with its task of
         // this round still to run) leave the round loop: every wave finishes
         // its own in a loop without barriers or task slots, each pixel held
@@ -1704,7 +1813,8 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     // multi-generation grid, while a grid that is resident all at once only
     // gets its expensive groups packed onto the same CUs (c3 at 1/8: 0.264
     // vs 0.243 ms with the order; 1/2: 0.493 vs 0.522)
-    bool feedback = SORTED && K.group_cost && K.group_order && grid <= K.order_cap;
+    // (the tail-mode instantiation runs without launch-order feedback)
+    bool feedback = SORTED && K.tail_n == 0 && K.group_cost && K.group_order && grid <= K.order_cap;
     if (feedback) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC>(), BLOCK,
@@ -1721,7 +1831,20 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     // brute-force scenes without quads: the quad tests compiled out
     const bool quads = BVH || K.n_quad > 0;
-    if (SORTED && feedback && quads)
+    bool tail_launched = false;
+    if constexpr (SORTED && !BVH && RT_TAIL) {
+        if (K.tail_n > 0) {
+            tail_launched = true;
+            if (quads)
+                hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, false, GREC, false, true, true>),
+                                   dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+            else
+                hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, false, GREC, false, false, true>),
+                                   dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+        }
+    }
+    if (tail_launched) {
+    } else if (SORTED && feedback && quads)
         hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, true>), dim3((unsigned)grid), dim3(BLOCK),
                            lds, stream, K);
     else if (SORTED && feedback)
@@ -1868,7 +1991,8 @@ bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
 size_t rt_render_rec_floats(const rt_kparams& K) {
     const long nitems = launch_items(K);
     const int lds_levels = K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS;
-    const size_t planes = (size_t)3 * (K.max_bounces - lds_levels);
+    // (+ the deepest level with the deferred fold, RT_DEFER_FOLD)
+    const size_t planes = (size_t)3 * (K.max_bounces - lds_levels + (RT_DEFER_FOLD ? 1 : 0));
     return planes ? planes * (size_t)((nitems + 255) / 256 * 256) : 1;
 }
 
