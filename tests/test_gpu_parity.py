@@ -757,6 +757,12 @@ def test_global_records_forced(bwrt_lib, oracle, monkeypatch, block, w, h, mb):
             img, st = run_pair(r, oracle, scenes.scene_07(), w, h, 3, mb, row_offset=off, row_stride=stride)
             assert np.array_equal(img, st.rgba)
             same_state(r, st)
+            # continuation (frames 4-5 in a second launch): the deferred fold
+            # of a launch's last frame happens inside that launch
+            img = r.render(w, h, 2, mb, first_frame=4, row_offset=off, row_stride=stride)
+            oracle.render(scenes.scene_07(), st, 2, mb, first_frame=4)
+            assert np.array_equal(img, st.rgba)
+            same_state(r, st)
     finally:
         r.close()
 
