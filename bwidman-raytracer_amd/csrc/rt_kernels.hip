@@ -388,7 +388,7 @@ __device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_
 // I-phase, where only the lanes whose path just ended run it (9.3 of 64
 // lanes per instruction, profiles/r04/check_a/phase_lanes.json)
 #ifndef RT_DEFER_FOLD
-#define RT_DEFER_FOLD 1
+#define RT_DEFER_FOLD 0  // off: measured slower (c3 0.79 vs 0.75 ms, c4 5.81 vs 5.50)
 #endif
 
 template <int BLOCK, bool HIT_LDS, bool BVH>
