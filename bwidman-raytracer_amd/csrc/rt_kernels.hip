@@ -944,9 +944,16 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
 // TAIL: the tail-mode instantiation (launched only when K.tail_n > 0: its
 // code costs the main loop spilled SGPRs even when no group enters it)
-template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true, bool TAIL = false>
+// OWN: pixels per workgroup (lanes 0 .. OWN-1 own one each; the others only
+// execute tasks).  OWN = BLOCK / 2 ("spread", small shards): a round's tasks
+// never fill more than half the queue, so the RANDDIR tasks (front) and the
+// SPEC tasks (back) land in different waves instead of one wave running both
+template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true, bool TAIL = false,
+          int OWN = BLOCK>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(!BVH && (GREC || TAIL) ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
+    static_assert(OWN == BLOCK || (!TAIL && OWN % 64 == 0 && OWN < BLOCK), "spread launches: no tail mode");
+    constexpr int RS = OWN;  // record-stack stride: one column per owner lane
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -977,8 +984,8 @@ rt_render_sorted_kernel(rt_kparams K) {
     // too, as level GL, so it outlives the round that made it
     constexpr bool DF = GREC && !BVH && RT_DEFER_FOLD;
     const int GLD = DF ? GL + 1 : GL;
-    float* grec = GREC ? K.rec + (long)blockIdx.x * 3 * GLD * BLOCK + tid : rec_base;
-    float* slots = rec_base + 3 * LL * BLOCK;
+    float* grec = GREC ? K.rec + (long)blockIdx.x * 3 * GLD * RS + tid : rec_base;
+    float* slots = rec_base + 3 * LL * RS;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
     // counters[0..3]: queue fronts/backs (2 parities)
     const long npix = (long)K.rows * K.width;
@@ -1006,7 +1013,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     const long group = ORDER && K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
     if (ORDER && tid == 0) K.group_cost[group] = (unsigned)__builtin_amdgcn_s_memrealtime();
     PixelState px;
-    load_item(K, npix, nitems, group * BLOCK + tid, px);
+    load_item(K, npix, nitems, tid < OWN ? group * OWN + tid : nitems, px);  // (lanes >= OWN: no pixel)
     int mode = px.passes_left > 0 ? T_REGEN : T_NONE;
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -1024,12 +1031,12 @@ rt_render_sorted_kernel(rt_kparams K) {
         const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
         if (GREC)
             for (int l = nrec - 1; l >= LL; --l) {
-                const float* r = grec + 3 * (l - LL) * BLOCK;
-                fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+                const float* r = grec + 3 * (l - LL) * RS;
+                fold_level(__float_as_int(r[0]), r[RS], r[2 * RS], hit_tab, lx, ly, lz);
             }
         for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-            const lds_float* r = rec + 3 * l * BLOCK;
-            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
+            const lds_float* r = rec + 3 * l * RS;
+            fold_level(__float_as_int(r[0]), r[RS], r[2 * RS], hit_tab, lx, ly, lz);
         }
 #if RT_PHASE_TWICE == 4
         {
@@ -1038,12 +1045,12 @@ rt_render_sorted_kernel(rt_kparams K) {
                 fold_level(__float_as_int(opq(SLOT(6, slot))), opq(SLOT(4, slot)), opq(SLOT(5, slot)), hit_tab, mx, my, mz);
             if (GREC)
                 for (int l = nrec - 1; l >= LL; --l) {
-                    const float* r = grec + 3 * (l - LL) * BLOCK;
-                    fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
+                    const float* r = grec + 3 * (l - LL) * RS;
+                    fold_level(__float_as_int(opq(r[0])), opq(r[RS]), opq(r[2 * RS]), hit_tab, mx, my, mz);
                 }
             for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-                const lds_float* r = rec + 3 * l * BLOCK;
-                fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
+                const lds_float* r = rec + 3 * l * RS;
+                fold_level(__float_as_int(opq(r[0])), opq(r[RS]), opq(r[2 * RS]), hit_tab, mx, my, mz);
             }
             keep(mx + my + mz);
         }
@@ -1208,21 +1215,21 @@ rt_render_sorted_kernel(rt_kparams K) {
                         // from its record stack: level max_bounces and the deep
                         // levels in global memory, the shallow ones in LDS
                         const int od = fv & 63, ot = (fv >> 6) & 1023;
-                        const float* gq = K.rec + (long)blockIdx.x * 3 * GLD * BLOCK + ot;
+                        const float* gq = K.rec + (long)blockIdx.x * 3 * GLD * RS + ot;
                         const lds_float* lq = (const lds_float*)(rec_base + ot);
                         float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
                         if (od > K.max_bounces) {
-                            const float* q = gq + 3 * GL * BLOCK;
-                            fold_level(__float_as_int(q[0]), q[BLOCK], q[2 * BLOCK], hit_tab, lx, ly, lz);
+                            const float* q = gq + 3 * GL * RS;
+                            fold_level(__float_as_int(q[0]), q[RS], q[2 * RS], hit_tab, lx, ly, lz);
                         }
                         const int nrec = od > K.max_bounces ? K.max_bounces : od;
                         for (int l = nrec - 1; l >= LL; --l) {
-                            const float* q = gq + 3 * (l - LL) * BLOCK;
-                            fold_level(__float_as_int(q[0]), q[BLOCK], q[2 * BLOCK], hit_tab, lx, ly, lz);
+                            const float* q = gq + 3 * (l - LL) * RS;
+                            fold_level(__float_as_int(q[0]), q[RS], q[2 * RS], hit_tab, lx, ly, lz);
                         }
                         for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-                            const lds_float* q = lq + 3 * l * BLOCK;
-                            fold_level(__float_as_int(q[0]), q[BLOCK], q[2 * BLOCK], hit_tab, lx, ly, lz);
+                            const lds_float* q = lq + 3 * l * RS;
+                            fold_level(__float_as_int(q[0]), q[RS], q[2 * RS], hit_tab, lx, ly, lz);
                         }
                         SLOT(4, tid) = lx;  // (slot fields 4..6 are free once read)
                         SLOT(5, tid) = ly;
@@ -1320,23 +1327,23 @@ rt_render_sorted_kernel(rt_kparams K) {
                 const float cosang = dot(d, hn);  // cosAngle, Main.cu:264
                 if (depth < K.max_bounces) {
                     if (!GREC || depth < LL) {  // (separate stores: LDS and global address spaces)
-                        lds_float* r = rec + 3 * depth * BLOCK;
+                        lds_float* r = rec + 3 * depth * RS;
                         r[0] = __int_as_float(code);
-                        r[BLOCK] = kspec;
-                        r[2 * BLOCK] = cosang;
+                        r[RS] = kspec;
+                        r[2 * RS] = cosang;
                     } else {
-                        float* r = grec + 3 * (depth - LL) * BLOCK;
+                        float* r = grec + 3 * (depth - LL) * RS;
                         r[0] = __int_as_float(code);
-                        r[BLOCK] = kspec;
-                        r[2 * BLOCK] = cosang;
+                        r[RS] = kspec;
+                        r[2 * RS] = cosang;
                     }
                     has_ray = true;  // from the hit point o along d
                 } else {  // next query would exceed maxBounces (Main.cu:210): the path ends
                     if (DF) {  // the deepest level: global level GL, folded next round
-                        float* r = grec + 3 * GL * BLOCK;
+                        float* r = grec + 3 * GL * RS;
                         r[0] = __int_as_float(code);
-                        r[BLOCK] = kspec;
-                        r[2 * BLOCK] = cosang;
+                        r[RS] = kspec;
+                        r[2 * RS] = cosang;
                     } else {
                         SLOT(4, slot) = kspec;
                         SLOT(5, slot) = cosang;
@@ -1775,17 +1782,25 @@ extern thread_local long rt_order_groups_last;
 hipError_t rt_launch_order_groups(const unsigned* cost, int* order, long n, hipStream_t stream);
 
 namespace {
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC>
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC, int OWN = BLOCK>
 void* kernel_ptr() {
-    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC>)
+    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, false, true, false, OWN>)
                   : reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
 }
 
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC = false>
+template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER, bool QUADS, bool TAIL, int OWN>
+void launch_sorted(const rt_kparams& K, long grid, size_t lds, hipStream_t stream) {
+    hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, ORDER, QUADS, TAIL, OWN>), dim3((unsigned)grid),
+                       dim3(BLOCK), lds, stream, K);
+}
+
+// OWN < BLOCK (sorted only): spread launch, OWN pixels per BLOCK-lane group
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC = false, int OWN = BLOCK>
 hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
+    static_assert(OWN == BLOCK || SORTED, "spread launches: sorted kernel only");
     rt_kparams K = K0;
     const long nitems = launch_items(K);
-    long grid = (nitems + BLOCK - 1) / BLOCK;  // streaming needs a resident grid only
+    long grid = (nitems + OWN - 1) / OWN;  // streaming needs a resident grid only
     if (grid_mult > 0 && !SORTED) {  // persistent (simple kernel): grid_mult x resident groups per CU x CUs
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC>(), BLOCK, lds) ==
@@ -1796,13 +1811,13 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
         }
     }
     if (grid < 1) grid = 1;
-    K.rec_stride = (int)(grid * BLOCK);
+    K.rec_stride = (int)(grid * OWN);
     // tail mode: brute-force scenes whose compiled records fit in the task-slot
     // area beside the hand-off record
     if (K.tail_n > 0) {
         const long nsc = (long)RT_SPH_FLOATS * K.n_sph + (long)RT_PLN_FLOATS * K.n_pln +
                          (long)RT_TRI_FLOATS * K.n_tri + (long)RT_QUAD_FLOATS * K.n_quad;
-        if (!SORTED || BVH || !RT_TAIL || (long)(BLOCK / 64) * RT_TAIL_FIELDS * RT_TAIL_MAX + nsc > 13L * BLOCK)
+        if (!SORTED || BVH || !RT_TAIL || OWN != BLOCK || (long)(BLOCK / 64) * RT_TAIL_FIELDS * RT_TAIL_MAX + nsc > 13L * BLOCK)
             K.tail_n = 0;
         if (K.tail_n > RT_TAIL_MAX) K.tail_n = RT_TAIL_MAX;
     }
@@ -1817,8 +1832,8 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     bool feedback = SORTED && K.tail_n == 0 && K.group_cost && K.group_order && grid <= K.order_cap;
     if (feedback) {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC>(), BLOCK,
-                                                         lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC, OWN>(),
+                                                         BLOCK, lds) != hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
         feedback = (double)grid > RT_ORDER_MIN_GEN * (double)per_cu * num_cus;
@@ -1831,33 +1846,27 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     // brute-force scenes without quads: the quad tests compiled out
     const bool quads = BVH || K.n_quad > 0;
-    bool tail_launched = false;
-    if constexpr (SORTED && !BVH && RT_TAIL) {
-        if (K.tail_n > 0) {
-            tail_launched = true;
-            if (quads)
-                hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, false, GREC, false, true, true>),
-                                   dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
-            else
-                hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, false, GREC, false, false, true>),
-                                   dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+    if constexpr (SORTED) {
+        if constexpr (!BVH && RT_TAIL && OWN == BLOCK) {
+            if (K.tail_n > 0) {
+                if (quads)
+                    launch_sorted<BLOCK, HIT_LDS, false, GREC, false, true, true, OWN>(K, grid, lds, stream);
+                else
+                    launch_sorted<BLOCK, HIT_LDS, false, GREC, false, false, true, OWN>(K, grid, lds, stream);
+                return hipGetLastError();  // (no launch-order feedback with the tail)
+            }
         }
-    }
-    if (tail_launched) {
-    } else if (SORTED && feedback && quads)
-        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, true>), dim3((unsigned)grid), dim3(BLOCK),
-                           lds, stream, K);
-    else if (SORTED && feedback)
-        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, true, false>), dim3((unsigned)grid),
-                           dim3(BLOCK), lds, stream, K);
-    else if (SORTED && quads)
-        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC>), dim3((unsigned)grid), dim3(BLOCK), lds,
-                           stream, K);
-    else if (SORTED)
-        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, false, false>), dim3((unsigned)grid),
-                           dim3(BLOCK), lds, stream, K);
-    else
+        if (feedback && quads)
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, true, false, OWN>(K, grid, lds, stream);
+        else if (feedback)
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, false, false, OWN>(K, grid, lds, stream);
+        else if (quads)
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, true, false, OWN>(K, grid, lds, stream);
+        else
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, false, false, OWN>(K, grid, lds, stream);
+    } else {
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+    }
     hipError_t e = hipGetLastError();
     // the sort runs when asked, and always for a grid without an order yet
     if (e == hipSuccess && feedback && (K0.order_sort || K0.order_n != grid)) {
@@ -1933,11 +1942,21 @@ hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, siz
                                 hipStream_t s);
 hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, int num_cus, hipStream_t s);
 
+size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted, int own = 0);
+
 namespace {
+// spread: the sorted kernel with BLOCK / 2 pixels per group (LDS records,
+// hit table in LDS, brute force only; other launches ignore it)
 template <int BLOCK, bool SORTED>
-hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s) {
+hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s,
+                        bool spread = false) {
     if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
         return rt_launch_render_bvh(K, BLOCK, SORTED, lds, grid_mult, num_cus, s);
+    if constexpr (SORTED && BLOCK >= 128) {
+        if (spread && hit_lds && !K.rec)
+            return launch_render<BLOCK, true, true, false, false, BLOCK / 2>(
+                K, rt_render_lds_bytes(K, BLOCK, true, true, BLOCK / 2), grid_mult, num_cus, s);
+    }
     if (SORTED && K.rec)  // record stack in global memory
         return hit_lds ? launch_render<BLOCK, true, SORTED, false, true>(K, lds, grid_mult, num_cus, s)
                        : launch_render<BLOCK, false, SORTED, false, true>(K, lds, grid_mult, num_cus, s);
@@ -1960,7 +1979,6 @@ hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_
 #ifndef RT_GREC_MIN_GEN
 #define RT_GREC_MIN_GEN 3.0
 #endif
-size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted);
 bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
     if (K.bvh_nodes || K.max_bounces <= 0) return false;
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
@@ -1997,14 +2015,15 @@ size_t rt_render_rec_floats(const rt_kparams& K) {
 }
 
 // LDS bytes of one workgroup: hit table (if staged) + 3 record dwords per
-// level per lane (+ 13 task-slot dwords per lane and 4 counters, sorted).
-size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted) {
+// level per owner lane (own: pixels per group, 0 = block) + 13 task-slot
+// dwords per lane and 8 counters (sorted).
+size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted, int own) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
     const int lds_levels = sorted && K.rec ? (K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS)
                                            : K.max_bounces + (sorted ? 0 : 1);
-    size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * block * sizeof(float);
+    size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * (own > 0 ? own : block) * sizeof(float);
     if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);  // + counters, tail threshold
     return b;
 }
@@ -2014,8 +2033,17 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 // sorted task-queue kernel unless `simple` (one pixel per lane: its grid
 // always covers every item); for the simple kernel grid_mult > 0 caps the
 // grid at grid_mult x resident workgroups per CU (persistent lanes).
+// spread_req: 1 / 0 forces the spread launch on / off (BWRT_SPREAD), -1 the
+// policy (RT_SPREAD_FEW: frames and shards of fewer than 4 full-size groups
+// per CU take 128-lane groups owning 64 pixels each: the c3 row shard of 1/8
+// 0.252 -> 0.227 ms, 1/16 0.254 -> 0.225; 256-lane groups owning 128: 0.233,
+// 0.234; the 1/4 shard, 4+ groups per CU, loses: 0.271 -> 0.332 ms;
+// profiles/r04/spread/ab_spread.txt, two alternating rounds)
+#ifndef RT_SPREAD_FEW
+#define RT_SPREAD_FEW 1
+#endif
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
-                            bool bvh_refill, hipStream_t stream) {
+                            bool bvh_refill, hipStream_t stream, int spread_req) {
     // samplesPerPixel > 1 (the reference's in-frame loop, off by default):
     // only the one-path-per-lane kernel implements it
     simple = simple || K.spp_inner > 1;
@@ -2039,9 +2067,11 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     if (block_req == 64 || block_req == 128 || block_req == 256) {  // explicit (BWRT_BLOCK)
         const size_t lds_r = rt_render_lds_bytes(K, block_req, hit_lds, true);
         if (lds_r <= 65536) {
+            const bool spread = spread_req > 0;
             if (block_req == 64) return launch_block<64, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
-            if (block_req == 128) return launch_block<128, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
-            return launch_block<256, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
+            if (block_req == 128)
+                return launch_block<128, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream, spread);
+            return launch_block<256, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream, spread);
         }
     }
     // BVH traversal: node-loop lengths differ widely between waves and a
@@ -2060,9 +2090,14 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     // small frames / shards (one rank of an 8-GPU frame): fewer than 4
     // full-size groups per CU leave CUs with unequal shares of the critical
     // path (every group is resident at once); 128-lane groups spread it
-    // (measured on c3 row shards of 1/8: 0.249 vs 0.264 ms; 1/4: 0.312 vs 0.291)
+    // (measured on c3 row shards of 1/8: 0.249 vs 0.264 ms; 1/4: 0.312 vs
+    // 0.291), and spread launches (above) spread it further
     const long items = (long)K.rows * K.width;
     const bool few_groups = items < (long)num_cus * 4 * RT_SORTED_BLOCK;
+    const bool spread = spread_req > 0 || (spread_req < 0 && RT_SPREAD_FEW && few_groups);
+    if (spread)  // (launch_block sizes a spread launch's LDS itself; this size is for those it cannot spread)
+        return launch_block<128, true>(K, hit_lds, rt_render_lds_bytes(K, 128, hit_lds, true), grid_mult, num_cus, stream,
+                                       true);
     if (RT_SORTED_BLOCK > 128 &&
         (few_groups ||
          waves_per_cu(rt_render_lds_bytes(K, 128, hit_lds, true), 128) > waves_per_cu(lds_s, RT_SORTED_BLOCK))) {

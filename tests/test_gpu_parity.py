@@ -789,6 +789,47 @@ def test_tail_mode_forced(bwrt_lib, oracle, monkeypatch, block, tail, grec):
         r.close()
 
 
+@pytest.mark.parametrize("block", [128, 256])
+def test_spread_launch_forced(bwrt_lib, oracle, monkeypatch, block):
+    """Spread launches (BWRT_SPREAD=1): block / 2 pixels per workgroup, the
+    other lanes only execute tasks, so a round's front (diffuse, regenerated)
+    and back (specular) tasks land in different waves.  Ragged sizes (the
+    last group part-owned), a one-pixel frame, row shards, quads, exact ties,
+    and a scene scaled by 1e10."""
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block)
+    cases = [(scenes.scene_07(), 160, 90, 3, 4, 0, 1), (scenes.scene_04_box(), 96, 61, 2, 5, 1, 3),
+             (_random_scene(7), 81, 45, 2, 6, 0, 1), (scenes.scene_07(), 1, 1, 2, 4, 0, 1),
+             (_scaled(_random_scene(3), 1e10), 64, 36, 2, 5, 0, 1)]
+    try:
+        for scene, w, h, spp, mb, off, stride in cases:
+            img, st = run_pair(r, oracle, scene, w, h, spp, mb, row_offset=off, row_stride=stride)
+            assert np.array_equal(img, st.rgba)
+            same_state(r, st)
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("block", [128, 256])
+def test_spread_launch_order_feedback(bwrt_lib, oracle, monkeypatch, block):
+    """A spread launch on a multi-generation grid (07 at 1080p, block / 2
+    pixels per group) with launch-order feedback: blockIdx order, then
+    reordered twice; every frame equals the oracle."""
+    w, h, mb = 1920, 1080, 4
+    scene = scenes.scene_07()
+    st = oracle.OracleState(w, h)
+    oracle.render(scene, st, 1, mb, first_frame=1)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block, BWRT_ORDER=1, BWRT_ORDER_PERIOD=2)
+    try:
+        r.set_scene(scene)
+        for _ in range(3):
+            r.init_rand(w, h)
+            img = r.render(w, h, 1, mb, first_frame=1)
+            assert np.array_equal(img, st.rgba)
+            same_state(r, st)
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("name", ["07", "04_box"])
 def test_simple_kernel_ab_reference(bwrt_lib, oracle, monkeypatch, name):
     """The one-path-per-lane kernel kept as the A/B reference (BWRT_KERNEL=simple)."""
