@@ -265,6 +265,15 @@ __device__ __forceinline__ void coop_step(float& bt, int& bk) {
     coop_pick(bt, bk, t2, k2);
 }
 
+// RT_KEY of a primitive id (spheres, planes, triangles, quads in turn); -1 for -1
+__device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
+    const int e_pln = K.n_sph, e_tri = e_pln + K.n_pln, e_quad = e_tri + K.n_tri;
+    return id < 0 ? -1
+                  : id < e_pln ? RT_KEY(0, id)
+                               : id < e_tri ? RT_KEY(1, id - e_pln)
+                                            : id < e_quad ? RT_KEY(2, id - e_tri) : RT_KEY(3, id - e_quad);
+}
+
 template <bool QUADS>
 __device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_float* sc, f3 o, f3 d, int sl, int S,
                                                  float& best_t, int& best_id) {
@@ -377,6 +386,11 @@ __device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_
 #endif
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
+#endif
+// spread launches of one owner wave: the executor wave takes half of every
+// closest hit (0 = off)
+#ifndef RT_SPLIT_HIT
+#define RT_SPLIT_HIT 1
 #endif
 // tail mode of the sorted kernel compiled in (K.tail_n turns it on per launch)
 #ifndef RT_TAIL
@@ -954,6 +968,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(!BVH
 rt_render_sorted_kernel(rt_kparams K) {
     static_assert(OWN == BLOCK || (!TAIL && OWN % 64 == 0 && OWN < BLOCK), "spread launches: no tail mode");
     constexpr int RS = OWN;  // record-stack stride: one column per owner lane
+    // split closest hits: one owner wave (its take-back reads and the ray
+    // posts are ordered within the wave) and one executor wave
+    constexpr bool SPLIT = !BVH && OWN == 64 && BLOCK == 128 && RT_SPLIT_HIT;
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1366,10 +1383,42 @@ rt_render_sorted_kernel(rt_kparams K) {
         }
 #endif
         // ---- I-phase: closest hit + brdfChoice (Main.cu:214-245)
+        // SPLIT (spread groups of one owner wave and one executor wave): the
+        // executor wave, idle here, takes half of every closest hit — the
+        // owner posts its ray in its own slot index (fields 0..3 and 7..12
+        // are free once the owner wave has taken its results back; 4..6 may
+        // hold a path's deepest level), each half tests every other index
+        // i of the reference's interleaved loop, and the owner keeps the
+        // smaller distance, ties to the larger key (the reference's result
+        // for rays that pass bvh_safe; the others take the whole loop)
+        bool split = false;
+        float t = INFINITY;
+        int id = -1;
+        if constexpr (SPLIT) {
+            if (tid < OWN) {
+                split = has_ray && bvh_safe(K, o, d);
+                SLOT(0, tid) = o.x;
+                SLOT(1, tid) = o.y;
+                SLOT(2, tid) = o.z;
+                SLOT(3, tid) = d.x;
+                SLOT(7, tid) = d.y;
+                SLOT(8, tid) = d.z;
+                SLOT(9, tid) = __int_as_float(split ? 1 : 0);
+            }
+            __syncthreads();
+            if (tid >= OWN) {
+                const int ot = tid - OWN;
+                if (__float_as_int(SLOT(9, ot))) {
+                    float t2;
+                    int id2;
+                    closest_hit_brute<QUADS, 2>(K, mk(SLOT(0, ot), SLOT(1, ot), SLOT(2, ot)),
+                                                mk(SLOT(3, ot), SLOT(7, ot), SLOT(8, ot)), t2, id2, 1);
+                    SLOT(10, ot) = t2;
+                    SLOT(11, ot) = __int_as_float(id2);
+                }
+            }
+        }
         if (has_ray) {
-            has_ray = false;
-            float t;
-            int id;
 #if RT_PHASE_TWICE == 1
             {
                 float t2;
@@ -1379,7 +1428,24 @@ rt_render_sorted_kernel(rt_kparams K) {
                 keep_i(id2);
             }
 #endif
-            closest_hit<BVH, QUADS>(K, o, d, t, id);
+            if (SPLIT && split)
+                closest_hit_brute<QUADS, 2>(K, o, d, t, id, 0);
+            else
+                closest_hit<BVH, QUADS>(K, o, d, t, id);
+        }
+        if constexpr (SPLIT) {
+            __syncthreads();
+            if (split) {  // the other half: smaller distance, ties to the larger key
+                const float t2 = SLOT(10, tid);
+                const int id2 = __float_as_int(SLOT(11, tid));
+                if (id2 >= 0 && (t2 < t || (t2 == t && prim_key(K, id2) > prim_key(K, id)))) {
+                    t = t2;
+                    id = id2;
+                }
+            }
+        }
+        if (has_ray) {
+            has_ray = false;
             if (id >= 0) {
                 const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
                 o = add(o, scale(t, d));  // the hit point: the next ray's origin

@@ -424,8 +424,11 @@ RT_HD void polygon_test(const rt_kparams& K, cfloat_ptr q, int nv, f3 o, f3 d, i
 // triangle i, quad i interleaved; acceptance `nearZero < t <= closest`.
 // QUADS = false: the scene has no quads (launch policy); the quad tests are
 // compiled out, which shortens the loop body (config 3: 0.871 -> 0.865 ms)
-template <bool QUADS = true>
-RT_HD void closest_hit_brute(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id) {
+// STEP = 2: only the indices i0, i0 + 2, ... (one half of a closest hit split
+// over two lanes, combined by key, rt_kernels.hip "split"; rays that pass
+// bvh_safe only)
+template <bool QUADS = true, int STEP = 1>
+RT_HD void closest_hit_brute(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id, int i0 = 0) {
     const float a = dot(d, d);
     const float a4 = 4.0f * a;
     const float a2 = 2.0f * a;
@@ -436,7 +439,7 @@ RT_HD void closest_hit_brute(const rt_kparams& K, f3 o, f3 d, float& best_t, int
     const int quad_base = tri_base + K.n_tri;
     const CullRay cr = cull_ray(K, o, d, a);
     RT_BRANCH_COUNT(K, 4);
-    for (int i = 0; i < K.n_max; i++) {
+    for (int i = i0; i < K.n_max; i += STEP) {
         if (i < K.n_sph) {  // Intersection.cuh:15-62
             const cfloat_ptr s = as_const(K.sph) + RT_SPH_FLOATS * i;
             f3 xp = mk(o.x - s[0], o.y - s[1], o.z - s[2]);
