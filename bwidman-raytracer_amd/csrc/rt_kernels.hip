@@ -2100,13 +2100,15 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 // always covers every item); for the simple kernel grid_mult > 0 caps the
 // grid at grid_mult x resident workgroups per CU (persistent lanes).
 // spread_req: 1 / 0 forces the spread launch on / off (BWRT_SPREAD), -1 the
-// policy (RT_SPREAD_FEW: frames and shards of fewer than 4 full-size groups
-// per CU take 128-lane groups owning 64 pixels each: the c3 row shard of 1/8
-// 0.252 -> 0.227 ms, 1/16 0.254 -> 0.225; 256-lane groups owning 128: 0.233,
-// 0.234; the 1/4 shard, 4+ groups per CU, loses: 0.271 -> 0.332 ms;
-// profiles/r04/spread/ab_spread.txt, two alternating rounds)
-#ifndef RT_SPREAD_FEW
-#define RT_SPREAD_FEW 1
+// policy: frames and shards of at most RT_SPREAD_PIX pixels per CU (about
+// 1.5 generations of the spread kernel's 7 waves per SIMD, 32 pixels per
+// wave) take 128-lane groups owning 64 pixels each.  Measured on c3 row
+// shards: 1/8 0.252 -> 0.227 ms, 1/16 0.254 -> 0.225 (256-lane groups owning
+// 128: 0.233, 0.234; profiles/r04/spread/ab_spread.txt); with the split
+// closest hit 1/6 (1,350 pixels per CU) 0.274 -> 0.248 but 1/4 (2,025) 0.270
+// -> 0.315 ms (profiles/r04/spread/ab_spread_mid.txt); 0 = off
+#ifndef RT_SPREAD_PIX
+#define RT_SPREAD_PIX 1400
 #endif
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
                             bool bvh_refill, hipStream_t stream, int spread_req) {
@@ -2160,7 +2162,7 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     // 0.291), and spread launches (above) spread it further
     const long items = (long)K.rows * K.width;
     const bool few_groups = items < (long)num_cus * 4 * RT_SORTED_BLOCK;
-    const bool spread = spread_req > 0 || (spread_req < 0 && RT_SPREAD_FEW && few_groups);
+    const bool spread = spread_req > 0 || (spread_req < 0 && items <= (long)num_cus * RT_SPREAD_PIX);
     if (spread)  // (launch_block sizes a spread launch's LDS itself; this size is for those it cannot spread)
         return launch_block<128, true>(K, hit_lds, rt_render_lds_bytes(K, 128, hit_lds, true), grid_mult, num_cus, stream,
                                        true);
