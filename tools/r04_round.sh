@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 profile set for the bench workload: GPU suite, smoke, bench with CPU
 # baseline, rocprofv3 kernel-trace stats of the bench, PMC passes, the traffic /
-# VALU summary bench.py reads, other configs' benches.  Each GPU step has its
+# VALU summary bench.py reads, other configs' benches, row-shard sweeps.  Each GPU step has its
 # own time limit; the chain stops at the first failure.
 # usage (GPU box, repo root): tools/r04_round.sh TAG
 set -o pipefail
@@ -21,5 +21,10 @@ python3 tools/make_traffic_json.py $OUT/pmc 07-1920x1080-8spp-4b-rows1 $OUT/traf
 for cfg in c2 c4 c5; do
   timeout -k 10 300 python bench.py --config $cfg > $OUT/bench_$cfg.log 2>&1 || { echo "bench $cfg failed"; tail -3 $OUT/bench_$cfg.log; exit 1; }
   echo "$cfg $(grep -o '"ms_per_step[^,]*' $OUT/bench_$cfg.log)"
+done
+export BWRT_TUNING=1  # shard_sweep forces BWRT_BLOCK=0 (the launch policy)
+for c in c3:1,2,4,8,16 c2:1,2,4,8,16 c4:2,4,8; do
+  timeout -k 10 200 python tools/shard_sweep.py --config ${c%:*} --strides ${c#*:} --blocks 0 --reps 20 > $OUT/shards_${c%:*}.txt 2>&1 || { echo "shards ${c%:*} failed"; tail -3 $OUT/shards_${c%:*}.txt; exit 1; }
+  grep stride $OUT/shards_${c%:*}.txt
 done
 echo done
