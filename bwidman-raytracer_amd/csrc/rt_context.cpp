@@ -31,7 +31,7 @@
 size_t rt_render_rec_floats(const rt_kparams& K);
 bool rt_render_wants_global_records(const rt_kparams& K, int num_cus);
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req, bool bvh_refill,
-                            hipStream_t stream, int spread_req);
+                            hipStream_t stream, int spread_req, int pair_req);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
                                hipStream_t stream);
 extern thread_local long rt_order_groups_last;
@@ -157,6 +157,7 @@ struct rt_context {
     int refill = -1;             // BWRT_REFILL: BVH refill kernel refill threshold (-1 = launch policy)
     int tail_n = -1;             // BWRT_TAIL: sorted-kernel tail-mode threshold (-1 = launch policy)
     int spread = -1;             // BWRT_SPREAD: 1 / 0 force the spread launch on / off (-1 = launch policy)
+    int pair = 1;                // BWRT_PAIR=0: spread launches through the sorted kernel instead of the pair kernel
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
     int spp_inner = 1;  // samplesPerPixel, Main.cu:27
@@ -910,6 +911,7 @@ int rt_create(int device, rt_context** out) {
     if (const char* g = tuning_env("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = tuning_env("BWRT_TAIL")) c->tail_n = std::min(std::max(std::atoi(g), 0), RT_TAIL_MAX);
     if (const char* g = tuning_env("BWRT_SPREAD")) c->spread = std::atoi(g) ? 1 : 0;
+    if (const char* g = tuning_env("BWRT_PAIR")) c->pair = std::atoi(g) ? 1 : 0;
     if (const char* g = tuning_env("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
     if (const char* g = tuning_env("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
     if (const char* g = tuning_env("BWRT_ORDER_PERIOD")) c->order_period = std::max(std::atoi(g), 1);
@@ -1640,7 +1642,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     // with kernel timing on, and one end event that serves both the ordering
     // of later calls (ev_render) and the timing
     if (c->ktiming) HIP_TRY(c, hipEventRecord(c->ev0, s));
-    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, s, c->spread);
+    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, s, c->spread, c->pair);
     if (e == hipSuccess && rt_order_groups_last > 0) c->order_n = rt_order_groups_last;
     c->launches++;
     if (gtimes && stamps) {

@@ -387,6 +387,11 @@ __device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
 #endif
+// occupancy target of the pair kernel
+#ifndef RT_PAIR_WAVES
+#define RT_PAIR_WAVES 7
+#endif
+
 // spread launches of one owner wave: the executor wave takes half of every
 // closest hit (0 = off)
 #ifndef RT_SPLIT_HIT
@@ -1558,6 +1563,283 @@ rt_render_sorted_kernel(rt_kparams K) {
 #undef RES
 }
 
+// ---- pair kernel (small frames and shards) --------------------------------
+// A 128-lane group of two waves for 64 pixels: wave 0 owns them (lane j
+// pixel j of the group's tile), wave 1 is their helper (lane 64 + j works
+// for owner j only), so no queue, no counters and no compaction — a wave
+// holds at most 64 tasks anyway.  A round (3 barriers):
+//   X  execute: the owner runs its pixel's diffuse bounce or camera ray in
+//      place (genRandomDirection, Main.cu:193-206, 290-292) and posts the
+//      next ray; the helper runs the owner's SPEC task (Main.cu:245-255) from
+//      its slot and posts that ray;
+//   H  closest hit (Main.cu:214-235): the owner takes its SPEC result back
+//      and records the bounce; owner and helper each test every other index
+//      i of the reference's interleaved loop on the posted ray (rays that
+//      fail bvh_safe: the whole loop on the owner);
+//   S  the owner keeps the smaller distance (ties to the larger RT_KEY),
+//      shades (Main.cu:237-245), folds and accumulates a finished path
+//      (Main.cu:262-268, 299-304) and posts a SPEC task.
+// Every pixel consumes its RNG stream in the reference's order, so results
+// equal the sorted kernel's and the oracle's bit for bit.
+// LDS: [hit table][records 3 x max_bounces x 64][exchange PF x 64][live flag]
+#define RT_PAIR_FIELDS 23
+template <bool HIT_LDS, bool ORDER, bool QUADS>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RT_PAIR_WAVES)))
+rt_render_pair_kernel(rt_kparams K) {
+    extern __shared__ float smem[];
+    const int tid = threadIdx.x;
+    const int j = tid & 63;           // the pixel this lane works for
+    const bool owner = tid < 64;      // (wave-uniform)
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    const float* hit_tab = K.hit;
+    float* rec_base = smem;
+    if (HIT_LDS) {
+        for (int i = tid; i < n_prim * RT_HIT_FLOATS; i += 128) smem[i] = K.hit[i];
+        hit_tab = smem;
+        rec_base = smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3);
+    }
+    const int levels = K.max_bounces;
+    // record stack [level][field][pixel] (the owner's only)
+    lds_float* rec = (lds_float*)(rec_base + j);
+    // exchange [field][pixel]: 0-2 ray origin, 3-5 ray direction, 6 ray flag
+    // (0 none, 1 split closest hit, 2 whole loop on the owner), 7-8 the
+    // helper's half (t, id); SPEC slot: 9-11 normal, 12-14 incoming direction
+    // in / scattered direction out, 15 primitive in / kspec out, 16-21 RNG
+    // state in / out, 22 SPEC flag (1 posted, 3 posted and its ray traced)
+    lds_float* xb = (lds_float*)(rec_base + 3 * levels * 64) + j;
+#define XF(f) xb[(f) * 64]
+    int* live_flag = reinterpret_cast<int*>(rec_base + 3 * levels * 64 + RT_PAIR_FIELDS * 64);
+    const long npix = (long)K.rows * K.width;
+    const long nitems = items_of(K, npix);
+#ifdef RT_GTIMES
+    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const long group = ORDER && K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
+    if (ORDER && tid == 0) K.group_cost[group] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    PixelState px;
+    load_item(K, npix, nitems, owner ? group * 64 + j : nitems, px);  // (helpers: no pixel)
+    int mode = px.passes_left > 0 ? T_REGEN : T_NONE;  // the owner's task this round
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f), hn = o;
+    int hid = 0, depth = 0;
+    const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
+    if (owner) XF(22) = __int_as_float(0);
+    __syncthreads();
+
+    while (true) {
+        // ---- X: execute
+        bool has_ray = false, ended = false;
+        int dcode = 0;              // deepest level (a bounce at depth max_bounces), folded at once
+        float dk = 0.0f, dc = 0.0f;
+        if (owner) {
+            if (mode == T_REGEN || mode == T_DIFF) {
+                f3 r = random_direction(px.rs, mode == T_REGEN ? px.d0 : hn);
+                if (mode == T_REGEN) {  // jittered camera ray, Main.cu:290-292
+                    d = normalize3(add(px.d0, scale(K.jitter, r)));
+                    o = cam;
+                    depth = 0;
+                    has_ray = true;
+                } else {  // diffuse bounce, Main.cu:257-264: brdf = 4 * albedo (fold)
+                    const float cosang = dot(r, hn);
+                    if (depth < K.max_bounces) {
+                        lds_float* q = rec + 3 * depth * 64;
+                        q[0] = __int_as_float(hid);
+                        q[64] = 0.0f;
+                        q[128] = cosang;
+                        d = r;
+                        has_ray = true;
+                    } else {
+                        dcode = hid;
+                        dc = cosang;
+                        ended = true;
+                    }
+                    depth++;
+                }
+            }
+            if (mode != T_SPEC) {  // (a SPEC lane's ray flag is the helper's)
+                const int flag = has_ray ? (bvh_safe(K, o, d) ? 1 : 2) : 0;
+                XF(0) = o.x;
+                XF(1) = o.y;
+                XF(2) = o.z;
+                XF(3) = d.x;
+                XF(4) = d.y;
+                XF(5) = d.z;
+                XF(6) = __int_as_float(flag);
+            }
+        } else {
+            const int sf = __float_as_int(XF(22));
+            if (sf & 1) {  // the owner's SPEC task, Main.cu:245-255
+                Xorwow rs;
+                rs.d = __float_as_uint(XF(16));
+                rs.v0 = __float_as_uint(XF(17));
+                rs.v1 = __float_as_uint(XF(18));
+                rs.v2 = __float_as_uint(XF(19));
+                rs.v3 = __float_as_uint(XF(20));
+                rs.v4 = __float_as_uint(XF(21));
+                const f3 nrm = mk(XF(9), XF(10), XF(11));
+                const f3 dd = mk(XF(12), XF(13), XF(14));
+                const int code = __float_as_int(XF(15));
+                const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
+                float kspec;
+                const f3 r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
+                XF(12) = r.x;
+                XF(13) = r.y;
+                XF(14) = r.z;
+                XF(15) = kspec;
+                XF(16) = __uint_as_float(rs.d);
+                XF(17) = __uint_as_float(rs.v0);
+                XF(18) = __uint_as_float(rs.v1);
+                XF(19) = __uint_as_float(rs.v2);
+                XF(20) = __uint_as_float(rs.v3);
+                XF(21) = __uint_as_float(rs.v4);
+                int flag = 0;
+                if (sf & 2) {  // traced: the ray from the hit point (posted in XF(0..2))
+                    XF(3) = r.x;
+                    XF(4) = r.y;
+                    XF(5) = r.z;
+                    flag = bvh_safe(K, mk(XF(0), XF(1), XF(2)), r) ? 1 : 2;
+                }
+                XF(6) = __int_as_float(flag);
+            }
+        }
+        __syncthreads();
+
+        // ---- H: SPEC take-back, closest hit halves
+        float t = INFINITY;
+        int id = -1;
+        int rflag = 0;
+        if (owner) {
+            if (mode == T_SPEC) {
+                const f3 r = mk(XF(12), XF(13), XF(14));
+                const float kspec = XF(15);
+                px.rs.d = __float_as_uint(XF(16));
+                px.rs.v0 = __float_as_uint(XF(17));
+                px.rs.v1 = __float_as_uint(XF(18));
+                px.rs.v2 = __float_as_uint(XF(19));
+                px.rs.v3 = __float_as_uint(XF(20));
+                px.rs.v4 = __float_as_uint(XF(21));
+                const float cosang = dot(r, hn);  // cosAngle, Main.cu:264
+                if (depth < K.max_bounces) {
+                    lds_float* q = rec + 3 * depth * 64;
+                    q[0] = __int_as_float(~hid);
+                    q[64] = kspec;
+                    q[128] = cosang;
+                    d = r;
+                    has_ray = true;
+                } else {
+                    dcode = ~hid;
+                    dk = kspec;
+                    dc = cosang;
+                    ended = true;
+                }
+                depth++;
+            }
+            if (has_ray) {
+                rflag = __float_as_int(XF(6));
+                if (rflag == 1)
+                    closest_hit_brute<QUADS, 2>(K, o, d, t, id, 0);
+                else
+                    closest_hit_brute<QUADS>(K, o, d, t, id);
+            }
+        } else if (__float_as_int(XF(6)) == 1) {
+            float t2;
+            int id2;
+            closest_hit_brute<QUADS, 2>(K, mk(XF(0), XF(1), XF(2)), mk(XF(3), XF(4), XF(5)), t2, id2, 1);
+            XF(7) = t2;
+            XF(8) = __int_as_float(id2);
+        }
+        __syncthreads();
+
+        // ---- S: merge, shade, fold, post
+        int live = 0;
+        if (owner) {
+            if (rflag == 1) {  // the helper's half: smaller distance, ties to the larger key
+                const float t2 = XF(7);
+                const int id2 = __float_as_int(XF(8));
+                if (id2 >= 0 && (t2 < t || (t2 == t && prim_key(K, id2) > prim_key(K, id)))) {
+                    t = t2;
+                    id = id2;
+                }
+            }
+            mode = T_NONE;
+            if (has_ray) {
+                if (id >= 0) {  // Main.cu:237-245
+                    const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
+                    o = add(o, scale(t, d));  // the hit point: the next ray's origin
+                    hn = mk(h0.x, h0.y, h0.z);
+                    if (h0.w != 0.0f) hn = normalize3(sub(o, hn));  // sphere normal
+                    hid = id;
+                    mode = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE ? T_SPEC : T_DIFF;  // brdfChoice
+                } else {
+                    ended = true;
+                }
+            }
+            if (ended) {  // fold innermost-first (Main.cu:262-268), accumulate (:299-304)
+                float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
+                if (depth > K.max_bounces) fold_level(dcode, dk, dc, hit_tab, lx, ly, lz);
+                const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
+                for (int l = nrec - 1; l >= 0; --l) {
+                    const lds_float* q = rec + 3 * l * 64;
+                    fold_level(__float_as_int(q[0]), q[64], q[128], hit_tab, lx, ly, lz);
+                }
+                if (px.frame == 1u) {
+                    px.ax = 0.0f;
+                    px.ay = 0.0f;
+                    px.az = 0.0f;
+                }
+                px.ax = px.ax + lx;
+                px.ay = px.ay + ly;
+                px.az = px.az + lz;
+                px.frame++;
+                px.passes_left--;
+                mode = px.passes_left > 0 ? T_REGEN : T_NONE;
+            }
+            int sf = 0;
+            if (mode == T_SPEC) {  // the helper's task next round
+                XF(9) = hn.x;
+                XF(10) = hn.y;
+                XF(11) = hn.z;
+                XF(12) = d.x;
+                XF(13) = d.y;
+                XF(14) = d.z;
+                XF(15) = __int_as_float(hid);
+                XF(16) = __uint_as_float(px.rs.d);
+                XF(17) = __uint_as_float(px.rs.v0);
+                XF(18) = __uint_as_float(px.rs.v1);
+                XF(19) = __uint_as_float(px.rs.v2);
+                XF(20) = __uint_as_float(px.rs.v3);
+                XF(21) = __uint_as_float(px.rs.v4);
+                sf = 1;
+                if (depth < K.max_bounces) {  // its scattered ray is traced from the hit point
+                    XF(0) = o.x;
+                    XF(1) = o.y;
+                    XF(2) = o.z;
+                    sf = 3;
+                }
+            }
+            XF(22) = __int_as_float(sf);
+            live = __ballot(mode != T_NONE) != 0ull;
+            if (j == 0) *live_flag = live;
+        }
+        __syncthreads();
+        if (!owner) live = *live_flag;
+        if (!live) break;  // (group-uniform)
+    }
+#undef XF
+    if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
+    if (ORDER && tid == 0) {
+        const volatile __attribute__((address_space(4))) rt_kparams* kp =
+            (const volatile __attribute__((address_space(4))) rt_kparams*)__builtin_amdgcn_kernarg_segment_ptr();
+        int* const ord = kp->group_order;
+        unsigned* const cost = kp->group_cost;
+        const long g = ord ? (long)__builtin_nontemporal_load(&ord[blockIdx.x]) : (long)blockIdx.x;
+        cost[g] = (unsigned)__builtin_amdgcn_s_memrealtime() - cost[g];
+    }
+#ifdef RT_GTIMES
+    __syncthreads();
+    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
 #ifdef RT_TU_BVH
 // ---- BVH kernel with ray refill (large scenes) --------------------------------
 // One path per lane like rt_render_kernel, but the BVH walk is not a
@@ -1848,21 +2130,27 @@ extern thread_local long rt_order_groups_last;
 hipError_t rt_launch_order_groups(const unsigned* cost, int* order, long n, hipStream_t stream);
 
 namespace {
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC, int OWN = BLOCK>
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC, int OWN = BLOCK, bool PAIR = false>
 void* kernel_ptr() {
+    if constexpr (PAIR) return reinterpret_cast<void*>(&rt_render_pair_kernel<HIT_LDS, false, true>);
     return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, false, true, false, OWN>)
                   : reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
 }
 
-template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER, bool QUADS, bool TAIL, int OWN>
+template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER, bool QUADS, bool TAIL, int OWN, bool PAIR = false>
 void launch_sorted(const rt_kparams& K, long grid, size_t lds, hipStream_t stream) {
-    hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, ORDER, QUADS, TAIL, OWN>), dim3((unsigned)grid),
-                       dim3(BLOCK), lds, stream, K);
+    if constexpr (PAIR)
+        hipLaunchKernelGGL((rt_render_pair_kernel<HIT_LDS, ORDER, QUADS>), dim3((unsigned)grid), dim3(128), lds, stream, K);
+    else
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, ORDER, QUADS, TAIL, OWN>),
+                           dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
 }
 
-// OWN < BLOCK (sorted only): spread launch, OWN pixels per BLOCK-lane group
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC = false, int OWN = BLOCK>
+// OWN < BLOCK (sorted only): spread launch, OWN pixels per BLOCK-lane group;
+// PAIR: the pair kernel (128 lanes, 64 pixels) instead of the sorted one
+template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC = false, int OWN = BLOCK, bool PAIR = false>
 hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
+    static_assert(!PAIR || (BLOCK == 128 && OWN == 64 && SORTED && !BVH && !GREC), "pair launches: 128 lanes, 64 pixels");
     static_assert(OWN == BLOCK || SORTED, "spread launches: sorted kernel only");
     rt_kparams K = K0;
     const long nitems = launch_items(K);
@@ -1898,11 +2186,14 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     bool feedback = SORTED && K.tail_n == 0 && K.group_cost && K.group_order && grid <= K.order_cap;
     if (feedback) {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC, OWN>(),
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC, OWN, PAIR>(),
                                                          BLOCK, lds) != hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
-        feedback = (double)grid > RT_ORDER_MIN_GEN * (double)per_cu * num_cus;
+        // (pair launches always: their grid is about one generation, and the
+        // order still helped there: c3 1/8 0.212 -> 0.206 ms, 1/16 0.187 ->
+        // 0.183, profiles/r04/spread/ab_pair.txt vs ab_prio.txt)
+        feedback = PAIR || (double)grid > RT_ORDER_MIN_GEN * (double)per_cu * num_cus;
     }
     if (!feedback) {
         K.group_cost = nullptr;
@@ -1923,13 +2214,13 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
             }
         }
         if (feedback && quads)
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, true, false, OWN>(K, grid, lds, stream);
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, true, false, OWN, PAIR>(K, grid, lds, stream);
         else if (feedback)
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, false, false, OWN>(K, grid, lds, stream);
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, false, false, OWN, PAIR>(K, grid, lds, stream);
         else if (quads)
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, true, false, OWN>(K, grid, lds, stream);
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, true, false, OWN, PAIR>(K, grid, lds, stream);
         else
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, false, false, OWN>(K, grid, lds, stream);
+            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, false, false, OWN, PAIR>(K, grid, lds, stream);
     } else {
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
     }
@@ -2009,15 +2300,26 @@ hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, siz
 hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, int num_cus, hipStream_t s);
 
 size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted, int own = 0);
+// LDS bytes of one pair-kernel group (hit table in LDS)
+size_t rt_pair_lds_bytes(const rt_kparams& K) {
+    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
+    return (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) +
+           (size_t)(3 * (K.max_bounces > 0 ? K.max_bounces : 0) + RT_PAIR_FIELDS) * 64 * sizeof(float) + 4 * sizeof(int);
+}
 
 namespace {
 // spread: the sorted kernel with BLOCK / 2 pixels per group (LDS records,
 // hit table in LDS, brute force only; other launches ignore it)
+// spread 2: the pair kernel where it applies (128-lane groups)
 template <int BLOCK, bool SORTED>
 hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s,
-                        bool spread = false) {
+                        int spread = 0) {
     if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
         return rt_launch_render_bvh(K, BLOCK, SORTED, lds, grid_mult, num_cus, s);
+    if constexpr (SORTED && BLOCK == 128) {
+        if (spread == 2 && hit_lds && !K.rec)
+            return launch_render<128, true, true, false, false, 64, true>(K, rt_pair_lds_bytes(K), grid_mult, num_cus, s);
+    }
     if constexpr (SORTED && BLOCK >= 128) {
         if (spread && hit_lds && !K.rec)
             return launch_render<BLOCK, true, true, false, false, BLOCK / 2>(
@@ -2111,7 +2413,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 #define RT_SPREAD_PIX 1400
 #endif
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
-                            bool bvh_refill, hipStream_t stream, int spread_req) {
+                            bool bvh_refill, hipStream_t stream, int spread_req, int pair_req) {
     // samplesPerPixel > 1 (the reference's in-frame loop, off by default):
     // only the one-path-per-lane kernel implements it
     simple = simple || K.spp_inner > 1;
@@ -2135,7 +2437,7 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     if (block_req == 64 || block_req == 128 || block_req == 256) {  // explicit (BWRT_BLOCK)
         const size_t lds_r = rt_render_lds_bytes(K, block_req, hit_lds, true);
         if (lds_r <= 65536) {
-            const bool spread = spread_req > 0;
+            const int spread = spread_req > 0 ? (pair_req && block_req == 128 ? 2 : 1) : 0;
             if (block_req == 64) return launch_block<64, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
             if (block_req == 128)
                 return launch_block<128, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream, spread);
@@ -2165,7 +2467,7 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     const bool spread = spread_req > 0 || (spread_req < 0 && items <= (long)num_cus * RT_SPREAD_PIX);
     if (spread)  // (launch_block sizes a spread launch's LDS itself; this size is for those it cannot spread)
         return launch_block<128, true>(K, hit_lds, rt_render_lds_bytes(K, 128, hit_lds, true), grid_mult, num_cus, stream,
-                                       true);
+                                       pair_req ? 2 : 1);
     if (RT_SORTED_BLOCK > 128 &&
         (few_groups ||
          waves_per_cu(rt_render_lds_bytes(K, 128, hit_lds, true), 128) > waves_per_cu(lds_s, RT_SORTED_BLOCK))) {

@@ -39,7 +39,7 @@
  *    result, only kernel choice and speed:
  *      at rt_create:    BWRT_KERNEL=simple, BWRT_BLOCK, BWRT_TILE, BWRT_TILE_SQ,
  *                       BWRT_GREC, BWRT_GRID_MULT, BWRT_LEAF_BATCH, BWRT_REFILL,
- *                       BWRT_TAIL, BWRT_SPREAD, BWRT_BVH_REFILL, BWRT_ORDER,
+ *                       BWRT_TAIL, BWRT_SPREAD, BWRT_PAIR, BWRT_BVH_REFILL, BWRT_ORDER,
  *                       BWRT_ORDER_PERIOD
  *      at rt_set_scene: BWRT_BVH_MIN, BWRT_BVH_LEAF, BWRT_BVH_CT, BWRT_BVH_SBVH,
  *                       BWRT_BVH_REFS, BWRT_BVH_ALPHA, BWRT_BVH_ORDER_MASK,

@@ -789,14 +789,16 @@ def test_tail_mode_forced(bwrt_lib, oracle, monkeypatch, block, tail, grec):
         r.close()
 
 
-@pytest.mark.parametrize("block", [128, 256])
-def test_spread_launch_forced(bwrt_lib, oracle, monkeypatch, block):
-    """Spread launches (BWRT_SPREAD=1): block / 2 pixels per workgroup, the
-    other lanes only execute tasks, so a round's front (diffuse, regenerated)
-    and back (specular) tasks land in different waves.  Ragged sizes (the
-    last group part-owned), a one-pixel frame, row shards, quads, exact ties,
-    and a scene scaled by 1e10."""
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block)
+@pytest.mark.parametrize("block,pair", [(128, 1), (128, 0), (256, 1)])
+def test_spread_launch_forced(bwrt_lib, oracle, monkeypatch, block, pair):
+    """Spread launches (BWRT_SPREAD=1): block / 2 pixels per workgroup.  128
+    lanes: the pair kernel (owner wave + helper wave: diffuse bounces in
+    place, SPEC tasks and half of every closest hit on the helper), or with
+    BWRT_PAIR=0 the sorted kernel with a split closest hit; 256 lanes: the
+    sorted kernel, two owner waves.  Ragged sizes (the last group
+    part-owned), a one-pixel frame, row shards, quads, exact ties, and a
+    scene scaled by 1e10 (rays that fail bvh_safe: the whole loop)."""
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block, BWRT_PAIR=pair)
     cases = [(scenes.scene_07(), 160, 90, 3, 4, 0, 1), (scenes.scene_04_box(), 96, 61, 2, 5, 1, 3),
              (_random_scene(7), 81, 45, 2, 6, 0, 1), (scenes.scene_07(), 1, 1, 2, 4, 0, 1),
              (_scaled(_random_scene(3), 1e10), 64, 36, 2, 5, 0, 1)]
@@ -809,8 +811,8 @@ def test_spread_launch_forced(bwrt_lib, oracle, monkeypatch, block):
         r.close()
 
 
-@pytest.mark.parametrize("block", [128, 256])
-def test_spread_launch_order_feedback(bwrt_lib, oracle, monkeypatch, block):
+@pytest.mark.parametrize("block,pair", [(128, 1), (128, 0), (256, 1)])
+def test_spread_launch_order_feedback(bwrt_lib, oracle, monkeypatch, block, pair):
     """A spread launch on a multi-generation grid (07 at 1080p, block / 2
     pixels per group) with launch-order feedback: blockIdx order, then
     reordered twice; every frame equals the oracle."""
@@ -818,7 +820,8 @@ def test_spread_launch_order_feedback(bwrt_lib, oracle, monkeypatch, block):
     scene = scenes.scene_07()
     st = oracle.OracleState(w, h)
     oracle.render(scene, st, 1, mb, first_frame=1)
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block, BWRT_ORDER=1, BWRT_ORDER_PERIOD=2)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block, BWRT_PAIR=pair, BWRT_ORDER=1,
+                        BWRT_ORDER_PERIOD=2)
     try:
         r.set_scene(scene)
         for _ in range(3):
