@@ -1625,12 +1625,34 @@ rt_render_pair_kernel(rt_kparams K) {
     if (owner) XF(22) = __int_as_float(0);
     __syncthreads();
 
+    bool fold = false;  // a finished path waits for its fold (run in the owner's X phase)
     while (true) {
         // ---- X: execute
         bool has_ray = false, ended = false;
-        int dcode = 0;              // deepest level (a bounce at depth max_bounces), folded at once
+        int dcode = 0;              // deepest level (a bounce at depth max_bounces)
         float dk = 0.0f, dc = 0.0f;
         if (owner) {
+            if (fold) {  // fold innermost-first (Main.cu:262-268), accumulate (:299-304)
+                fold = false;
+                float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
+                if (depth > K.max_bounces)  // (the deepest level, parked in XF(6..8))
+                    fold_level(__float_as_int(XF(6)), XF(7), XF(8), hit_tab, lx, ly, lz);
+                const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
+                for (int l = nrec - 1; l >= 0; --l) {
+                    const lds_float* q = rec + 3 * l * 64;
+                    fold_level(__float_as_int(q[0]), q[64], q[128], hit_tab, lx, ly, lz);
+                }
+                if (px.frame == 1u) {
+                    px.ax = 0.0f;
+                    px.ay = 0.0f;
+                    px.az = 0.0f;
+                }
+                px.ax = px.ax + lx;
+                px.ay = px.ay + ly;
+                px.az = px.az + lz;
+                px.frame++;
+                px.passes_left--;
+            }
             if (mode == T_REGEN || mode == T_DIFF) {
                 f3 r = random_direction(px.rs, mode == T_REGEN ? px.d0 : hn);
                 if (mode == T_REGEN) {  // jittered camera ray, Main.cu:290-292
@@ -1773,25 +1795,15 @@ rt_render_pair_kernel(rt_kparams K) {
                     ended = true;
                 }
             }
-            if (ended) {  // fold innermost-first (Main.cu:262-268), accumulate (:299-304)
-                float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
-                if (depth > K.max_bounces) fold_level(dcode, dk, dc, hit_tab, lx, ly, lz);
-                const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
-                for (int l = nrec - 1; l >= 0; --l) {
-                    const lds_float* q = rec + 3 * l * 64;
-                    fold_level(__float_as_int(q[0]), q[64], q[128], hit_tab, lx, ly, lz);
-                }
-                if (px.frame == 1u) {
-                    px.ax = 0.0f;
-                    px.ay = 0.0f;
-                    px.az = 0.0f;
-                }
-                px.ax = px.ax + lx;
-                px.ay = px.ay + ly;
-                px.az = px.az + lz;
-                px.frame++;
-                px.passes_left--;
-                mode = px.passes_left > 0 ? T_REGEN : T_NONE;
+            if (ended) {
+                // the fold runs in the next X phase, beside the helper's SPEC
+                // tasks (the longer half of X); the deepest level waits in
+                // XF(6..8), free until the owner posts its next ray there
+                fold = true;
+                XF(6) = __int_as_float(dcode);
+                XF(7) = dk;
+                XF(8) = dc;
+                mode = px.passes_left > 1 ? T_REGEN : T_NONE;
             }
             int sf = 0;
             if (mode == T_SPEC) {  // the helper's task next round
@@ -1817,7 +1829,7 @@ rt_render_pair_kernel(rt_kparams K) {
                 }
             }
             XF(22) = __int_as_float(sf);
-            live = __ballot(mode != T_NONE) != 0ull;
+            live = __ballot(mode != T_NONE || fold) != 0ull;
             if (j == 0) *live_flag = live;
         }
         __syncthreads();
