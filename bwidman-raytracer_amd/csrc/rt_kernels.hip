@@ -1574,8 +1574,9 @@ rt_render_sorted_kernel(rt_kparams K) {
 //      its slot and posts that ray;
 //   H  closest hit (Main.cu:214-235): the owner takes its SPEC result back
 //      and records the bounce; owner and helper each test every other index
-//      i of the reference's interleaved loop on the posted ray (rays that
-//      fail bvh_safe: the whole loop on the owner);
+//      i of the reference's interleaved loop on the posted ray, the helper
+//      the even ones (index 0 carries the planes), the owner the odd ones
+//      (rays that fail bvh_safe: the whole loop on the owner);
 //   S  the owner keeps the smaller distance (ties to the larger RT_KEY),
 //      shades (Main.cu:237-245), folds and accumulates a finished path
 //      (Main.cu:262-268, 299-304) and posts a SPEC task.
@@ -1757,15 +1758,15 @@ rt_render_pair_kernel(rt_kparams K) {
             }
             if (has_ray) {
                 rflag = __float_as_int(XF(6));
-                if (rflag == 1)
-                    closest_hit_brute<QUADS, 2>(K, o, d, t, id, 0);
+                if (rflag == 1)  // (the odd indices: the owner also took its SPEC result back)
+                    closest_hit_brute<QUADS, 2>(K, o, d, t, id, 1);
                 else
                     closest_hit_brute<QUADS>(K, o, d, t, id);
             }
         } else if (__float_as_int(XF(6)) == 1) {
             float t2;
             int id2;
-            closest_hit_brute<QUADS, 2>(K, mk(XF(0), XF(1), XF(2)), mk(XF(3), XF(4), XF(5)), t2, id2, 1);
+            closest_hit_brute<QUADS, 2>(K, mk(XF(0), XF(1), XF(2)), mk(XF(3), XF(4), XF(5)), t2, id2, 0);
             XF(7) = t2;
             XF(8) = __int_as_float(id2);
         }
