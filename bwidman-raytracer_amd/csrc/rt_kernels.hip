@@ -1577,13 +1577,15 @@ rt_render_sorted_kernel(rt_kparams K) {
 //      i of the reference's interleaved loop on the posted ray, the helper
 //      the even ones (index 0 carries the planes), the owner the odd ones
 //      (rays that fail bvh_safe: the whole loop on the owner);
-//   S  the owner keeps the smaller distance (ties to the larger RT_KEY),
-//      shades (Main.cu:237-245), folds and accumulates a finished path
-//      (Main.cu:262-268, 299-304) and posts a SPEC task.
+//   S  owner and helper merge the halves the same way (the smaller
+//      distance, ties to the larger RT_KEY); the helper computes the hit
+//      point and normal (Main.cu:237-241) for both, the owner draws
+//      brdfChoice (:243), parks a finished path for its fold in the next X
+//      phase (Main.cu:262-268, 299-304) and posts a SPEC task.
 // Every pixel consumes its RNG stream in the reference's order, so results
 // equal the sorted kernel's and the oracle's bit for bit.
 // LDS: [hit table][records 3 x max_bounces x 64][exchange PF x 64][live flag]
-#define RT_PAIR_FIELDS 23
+#define RT_PAIR_FIELDS 25
 template <bool HIT_LDS, bool ORDER, bool QUADS>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(RT_PAIR_WAVES)))
 rt_render_pair_kernel(rt_kparams K) {
@@ -1602,11 +1604,13 @@ rt_render_pair_kernel(rt_kparams K) {
     const int levels = K.max_bounces;
     // record stack [level][field][pixel] (the owner's only)
     lds_float* rec = (lds_float*)(rec_base + j);
-    // exchange [field][pixel]: 0-2 ray origin, 3-5 ray direction, 6 ray flag
-    // (0 none, 1 split closest hit, 2 whole loop on the owner), 7-8 the
-    // helper's half (t, id); SPEC slot: 9-11 normal, 12-14 incoming direction
-    // in / scattered direction out, 15 primitive in / kspec out, 16-21 RNG
-    // state in / out, 22 SPEC flag (1 posted, 3 posted and its ray traced)
+    // exchange [field][pixel]: 0-2 ray origin (in S the helper overwrites it
+    // with the hit point), 3-5 ray direction, 6 ray flag (0 none, 1 split
+    // closest hit, 2 whole loop on the owner), 7-8 the helper's half (t, id),
+    // 9-11 the hit's normal (written by the helper in S), 12-14 SPEC
+    // scattered direction out, 15 SPEC kspec out, 16-21 RNG state (SPEC in /
+    // out), 22 SPEC flag (1 posted, 3 posted and its ray traced), 23-24 the
+    // owner's (t, id)
     lds_float* xb = (lds_float*)(rec_base + 3 * levels * 64) + j;
 #define XF(f) xb[(f) * 64]
     int* live_flag = reinterpret_cast<int*>(rec_base + 3 * levels * 64 + RT_PAIR_FIELDS * 64);
@@ -1622,6 +1626,8 @@ rt_render_pair_kernel(rt_kparams K) {
     int mode = px.passes_left > 0 ? T_REGEN : T_NONE;  // the owner's task this round
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f), hn = o;
     int hid = 0, depth = 0;
+    bool hit = false;   // (owner) last S found a hit: its point and normal come from the helper
+    int hflag = 0;      // (helper) the ray flag of this round
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
     if (owner) XF(22) = __int_as_float(0);
     __syncthreads();
@@ -1653,6 +1659,11 @@ rt_render_pair_kernel(rt_kparams K) {
                 px.az = px.az + lz;
                 px.frame++;
                 px.passes_left--;
+            }
+            if (hit) {  // the hit point and normal the helper computed in S
+                hit = false;
+                o = mk(XF(0), XF(1), XF(2));
+                hn = mk(XF(9), XF(10), XF(11));
             }
             if (mode == T_REGEN || mode == T_DIFF) {
                 f3 r = random_direction(px.rs, mode == T_REGEN ? px.d0 : hn);
@@ -1699,9 +1710,8 @@ rt_render_pair_kernel(rt_kparams K) {
                 rs.v3 = __float_as_uint(XF(20));
                 rs.v4 = __float_as_uint(XF(21));
                 const f3 nrm = mk(XF(9), XF(10), XF(11));
-                const f3 dd = mk(XF(12), XF(13), XF(14));
-                const int code = __float_as_int(XF(15));
-                const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
+                const f3 dd = mk(XF(3), XF(4), XF(5));  // the incoming ray
+                const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * hid + 8);
                 float kspec;
                 const f3 r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
                 XF(12) = r.x;
@@ -1762,13 +1772,16 @@ rt_render_pair_kernel(rt_kparams K) {
                     closest_hit_brute<QUADS, 2>(K, o, d, t, id, 1);
                 else
                     closest_hit_brute<QUADS>(K, o, d, t, id);
+                XF(23) = t;
+                XF(24) = __int_as_float(id);
             }
-        } else if (__float_as_int(XF(6)) == 1) {
-            float t2;
-            int id2;
-            closest_hit_brute<QUADS, 2>(K, mk(XF(0), XF(1), XF(2)), mk(XF(3), XF(4), XF(5)), t2, id2, 0);
-            XF(7) = t2;
-            XF(8) = __int_as_float(id2);
+        } else {
+            hflag = __float_as_int(XF(6));
+            if (hflag == 1) {
+                closest_hit_brute<QUADS, 2>(K, mk(XF(0), XF(1), XF(2)), mk(XF(3), XF(4), XF(5)), t, id, 0);
+                XF(7) = t;
+                XF(8) = __int_as_float(id);
+            }
         }
         __syncthreads();
 
@@ -1785,12 +1798,9 @@ rt_render_pair_kernel(rt_kparams K) {
             }
             mode = T_NONE;
             if (has_ray) {
-                if (id >= 0) {  // Main.cu:237-245
-                    const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
-                    o = add(o, scale(t, d));  // the hit point: the next ray's origin
-                    hn = mk(h0.x, h0.y, h0.z);
-                    if (h0.w != 0.0f) hn = normalize3(sub(o, hn));  // sphere normal
+                if (id >= 0) {  // Main.cu:237-245 (the helper computes the point and normal)
                     hid = id;
+                    hit = true;
                     mode = rand_range(px.rs, 1.0f) < RT_SPECULAR_CHANCE ? T_SPEC : T_DIFF;  // brdfChoice
                 } else {
                     ended = true;
@@ -1807,31 +1817,41 @@ rt_render_pair_kernel(rt_kparams K) {
                 mode = px.passes_left > 1 ? T_REGEN : T_NONE;
             }
             int sf = 0;
-            if (mode == T_SPEC) {  // the helper's task next round
-                XF(9) = hn.x;
-                XF(10) = hn.y;
-                XF(11) = hn.z;
-                XF(12) = d.x;
-                XF(13) = d.y;
-                XF(14) = d.z;
-                XF(15) = __int_as_float(hid);
+            if (mode == T_SPEC) {  // the helper's task next round (its hit, normal and ray it has)
                 XF(16) = __uint_as_float(px.rs.d);
                 XF(17) = __uint_as_float(px.rs.v0);
                 XF(18) = __uint_as_float(px.rs.v1);
                 XF(19) = __uint_as_float(px.rs.v2);
                 XF(20) = __uint_as_float(px.rs.v3);
                 XF(21) = __uint_as_float(px.rs.v4);
-                sf = 1;
-                if (depth < K.max_bounces) {  // its scattered ray is traced from the hit point
-                    XF(0) = o.x;
-                    XF(1) = o.y;
-                    XF(2) = o.z;
-                    sf = 3;
-                }
+                sf = depth < K.max_bounces ? 3 : 1;  // 3: its scattered ray is traced from the hit point
             }
             XF(22) = __int_as_float(sf);
             live = __ballot(mode != T_NONE || fold) != 0ull;
             if (j == 0) *live_flag = live;
+        } else if (hflag != 0) {
+            // the same merge as the owner's, then the hit point and normal
+            // (Main.cu:237-241; the same float operations), for the owner's
+            // next X phase and the SPEC task
+            float tt = XF(23);
+            int ii = __float_as_int(XF(24));
+            if (hflag == 1 && id >= 0 && (t < tt || (t == tt && prim_key(K, id) > prim_key(K, ii)))) {
+                tt = t;
+                ii = id;
+            }
+            if (ii >= 0) {
+                const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * ii);
+                const f3 hp = add(mk(XF(0), XF(1), XF(2)), scale(tt, mk(XF(3), XF(4), XF(5))));
+                f3 nn = mk(h0.x, h0.y, h0.z);
+                if (h0.w != 0.0f) nn = normalize3(sub(hp, nn));  // sphere normal
+                XF(0) = hp.x;
+                XF(1) = hp.y;
+                XF(2) = hp.z;
+                XF(9) = nn.x;
+                XF(10) = nn.y;
+                XF(11) = nn.z;
+                hid = ii;
+            }
         }
         __syncthreads();
         if (!owner) live = *live_flag;
