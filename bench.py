@@ -18,13 +18,18 @@ ms/frame = ms_per_step.
 The CPU baseline is the library's scalar C++ fallback (rt_render_cpu) on
 every CPU of the process's affinity (or --cpu-threads), timed on rank 0 at
 N = 1 after the GPU steps, and checked bit-exact against the GPU.
-For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+N > 1: one rank per GPU over RCCL.  Under torch.distributed.run (WORLD_SIZE
+set) each process is one rank; a plain `python bench.py --gpus N` starts
+torch.distributed.run itself (N child ranks on 127.0.0.1) before touching
+the GPU, forwards their output and exits with their status.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -135,14 +140,39 @@ def load_traffic(path, workload_key):
     return None
 
 
+def self_launch_command(argv, nproc, port):
+    """The command and environment that run this script as `nproc` ranks of
+    torch.distributed.run on this node (rendezvous on 127.0.0.1:port), with
+    the same arguments; each rank then reads RANK / LOCAL_RANK / WORLD_SIZE."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"  # dmabuf IPC: RCCL needs it on this driver
+    env.setdefault("OMP_NUM_THREADS", "1")  # torch.distributed.run would print a warning and set it
+    return cmd, env
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # a plain launch for N GPUs: start the N ranks as children.  Nothing
+        # here has touched the GPU (importing torch does not), and this
+        # process only waits for them: no exec, no retry
+        cmd, env = self_launch_command(sys.argv[1:], args.gpus, free_port())
+        print(f"bench: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+        raise SystemExit(subprocess.run(cmd, env=env).returncode)
     scene_key, W, H, SPP, MB, _ = scenes.CONFIGS[args.config]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # one process per GPU (LOCAL_RANK); the modulo only matters when ranks
     # are rehearsed on fewer GPUs than ranks (BWRT_DIST_BACKEND=gloo)
     dev_index = local % max(torch.cuda.device_count(), 1)

@@ -126,6 +126,7 @@ def _proto(lib):
         "rt_set_state": (C.c_int, [vp, vp, vp, C.c_uint]),
         "rt_error_string": (C.c_char_p, [C.c_int]),
         "rt_last_error": (C.c_char_p, [vp]),
+        "rt_last_kernel_name": (C.c_char_p, [vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

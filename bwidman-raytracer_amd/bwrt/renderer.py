@@ -160,6 +160,10 @@ class Renderer:
     def last_kernel_ms(self) -> float:
         return self.lib.rt_last_kernel_ms(self.ctx)
 
+    def last_kernel_name(self) -> str:
+        """The render kernel the last GPU render launched (rt_last_kernel_name)."""
+        return self.lib.rt_last_kernel_name(self.ctx).decode()
+
     def set_kernel_timing(self, enable: bool):
         """Per-launch timing events for last_kernel_ms (rt_set_kernel_timing)."""
         self._check(self.lib.rt_set_kernel_timing(self.ctx, int(bool(enable))))

@@ -30,11 +30,12 @@
 
 size_t rt_render_rec_floats(const rt_kparams& K);
 bool rt_render_wants_global_records(const rt_kparams& K, int num_cus);
-hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req, bool bvh_refill,
-                            hipStream_t stream, int spread_req, int pair_req);
+hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
+                            hipStream_t stream, int pair_req);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
                                hipStream_t stream);
 extern thread_local long rt_order_groups_last;
+extern thread_local char rt_launched_kernel[96];
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
                                   int shards, int rows_per_shard, hipStream_t stream);
 // scalar C++ CPU fallback (rt_cpu.cpp)
@@ -81,7 +82,6 @@ struct rt_context {
     int device = 0;
     int num_cus = 256;
     bool simple = false;  // BWRT_KERNEL=simple: one-path-per-lane kernel (A/B reference)
-    bool bvh_refill = true;  // BWRT_BVH_REFILL=0: BVH scenes through the sorted kernel instead
     int grid_mult = 0;  // persistent grid = grid_mult x resident workgroups per CU x CUs
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr;  // start of the last render (timing)
@@ -155,9 +155,8 @@ struct rt_context {
     int tile_sq = 0;             // BWRT_TILE_SQ: a 4-wave group's tiles as 2 x 2 (experiment)
     int leaf_batch = -1;         // BWRT_LEAF_BATCH: BVH refill kernel leaf-batch threshold (-1 = launch policy)
     int refill = -1;             // BWRT_REFILL: BVH refill kernel refill threshold (-1 = launch policy)
-    int tail_n = -1;             // BWRT_TAIL: sorted-kernel tail-mode threshold (-1 = launch policy)
-    int spread = -1;             // BWRT_SPREAD: 1 / 0 force the spread launch on / off (-1 = launch policy)
-    int pair = 1;                // BWRT_PAIR=0: spread launches through the sorted kernel instead of the pair kernel
+    int spread = -1;             // BWRT_SPREAD: 1 / 0 force the pair kernel on / off (-1 = launch policy)
+    std::string kernel_name;     // the render kernel of the last launch (rt_last_kernel_name)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
     int spp_inner = 1;  // samplesPerPixel, Main.cu:27
@@ -165,7 +164,7 @@ struct rt_context {
 
 namespace {
 
-// Tuning and diagnostic knobs (BWRT_BLOCK, BWRT_TILE, BWRT_GREC, BWRT_TAIL,
+// Tuning and diagnostic knobs (BWRT_BLOCK, BWRT_TILE, BWRT_GREC, BWRT_SPREAD,
 // BWRT_ORDER*, BWRT_BVH_*, BWRT_STAMPS, ...; listed in rt_abi.h) are read
 // only when the process sets BWRT_TUNING=1: a default context always takes
 // the measured launch policy, whatever else the environment holds.
@@ -909,10 +908,7 @@ int rt_create(int device, rt_context** out) {
     if (const char* g = tuning_env("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
     if (const char* g = tuning_env("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = tuning_env("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
-    if (const char* g = tuning_env("BWRT_TAIL")) c->tail_n = std::min(std::max(std::atoi(g), 0), RT_TAIL_MAX);
     if (const char* g = tuning_env("BWRT_SPREAD")) c->spread = std::atoi(g) ? 1 : 0;
-    if (const char* g = tuning_env("BWRT_PAIR")) c->pair = std::atoi(g) ? 1 : 0;
-    if (const char* g = tuning_env("BWRT_BVH_REFILL")) c->bvh_refill = std::atoi(g) != 0;
     if (const char* g = tuning_env("BWRT_ORDER")) c->order_feedback = std::atoi(g) != 0;
     if (const char* g = tuning_env("BWRT_ORDER_PERIOD")) c->order_period = std::max(std::atoi(g), 1);
     *out = c;
@@ -1588,7 +1584,6 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     // ends with the slowest waves) batch later
     K.leaf_batch = c->leaf_batch > 0 ? c->leaf_batch : small ? RT_LEAF_BATCH_SMALL : RT_LEAF_BATCH;
     K.refill = c->refill > 0 ? c->refill : small ? RT_REFILL_SMALL : RT_REFILL;
-    K.tail_n = c->tail_n >= 0 ? c->tail_n : RT_TAIL_N;
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
     if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K, c->num_cus)))) {
@@ -1597,7 +1592,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.rec = (float*)c->rec.p;
     }
     unsigned long long* stamps = nullptr;
-    const int NST = 40;  // 8 per-phase wave-cycle sums + utilisation / branch counters + tail
+    const int NST = 40;  // 8 per-phase wave-cycle sums + utilisation / branch counters
     if (tuning_env("BWRT_STAMPS")) {  // diagnostic builds (-DRT_STAMPS)
         if (hipMalloc(&stamps, NST * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemsetAsync(stamps, 0, NST * sizeof(unsigned long long), s);
@@ -1637,13 +1632,15 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         HIP_TRY(c, hipStreamWaitEvent(s, c->ev_render, 0));
     }
     rt_order_groups_last = 0;
+    rt_launched_kernel[0] = 0;
     // every event recorded here is a marker packet the GPU drains between two
     // renders (~5 us each on MI355X, tools/ev_ab.sh): the start marker only
     // with kernel timing on, and one end event that serves both the ordering
     // of later calls (ev_render) and the timing
     if (c->ktiming) HIP_TRY(c, hipEventRecord(c->ev0, s));
-    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, c->bvh_refill, s, c->spread, c->pair);
+    hipError_t e = rt_launch_render(K, c->num_cus, c->grid_mult, c->simple, c->block, s, c->spread);
     if (e == hipSuccess && rt_order_groups_last > 0) c->order_n = rt_order_groups_last;
+    c->kernel_name = rt_launched_kernel;
     c->launches++;
     if (gtimes && stamps) {
         std::vector<unsigned long long> h(NGT);
@@ -1806,8 +1803,10 @@ int rt_synchronize(rt_context* c) {
     if (!c) return RT_ERR_INVALID_ARGUMENT;
     if (c->cpu) return RT_OK;  // CPU renders are synchronous
     HIP_TRY(c, hipSetDevice(c->device));
+    // record a deferred end event first, so ev_render always marks the last
+    // render (later renders on a caller's stream wait on it)
+    HIP_TRY(c, flush_render(c));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    c->render_pending = false;  // a deferred end event's launch is done too
     if (c->render_recorded) HIP_TRY(c, hipEventSynchronize(c->ev_render));
     if (c->aux_recorded) HIP_TRY(c, hipEventSynchronize(c->ev_aux));
     return RT_OK;
@@ -1910,6 +1909,8 @@ const char* rt_error_string(int status) {
 }
 
 const char* rt_last_error(const rt_context* c) { return c ? c->err.c_str() : ""; }
+
+const char* rt_last_kernel_name(const rt_context* c) { return c ? c->kernel_name.c_str() : ""; }
 
 int rt_render_cpu(rt_context* c, const rt_render_params* p, int threads, uint8_t* rgba_out, float* accum_out) {
     if (!c) return RT_ERR_INVALID_ARGUMENT;

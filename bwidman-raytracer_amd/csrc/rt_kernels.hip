@@ -31,6 +31,8 @@
 //    per-ray math, not a contraction).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "rt_layout.h"
 #include "rt_path.h"
 
@@ -232,39 +234,6 @@ __device__ __forceinline__ Xorwow opq_rs(Xorwow r) {
     return q;
 }
 
-// ---- tail mode: one closest hit split over a segment of S lanes -----------
-// (S = 2, 4, 8 or 16 aligned lanes that hold the same ray).  Lane sl of the
-// segment tests primitives j = sl, sl + S, ... of the list [spheres, planes,
-// triangles, quads] with the reference's arithmetic (closest_hit_brute's
-// tests, records staged in LDS), keeping the best (t, RT_KEY) by key_accept;
-// the segment then reduces its lanes' bests with DPP (quad xor 1, quad xor 2,
-// row half-mirror, row mirror: every step stays inside an aligned segment).
-// The result is the minimum distance with ties to the largest key, which is
-// what the reference's interleaved `t > closest` loop (Main.cu:217-234)
-// returns for rays whose tests cannot produce a NaN distance (bvh_safe); the
-// caller sends the other rays through closest_hit_brute.
-typedef float v4f __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4f lds_v4f;
-
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) {
-    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false);
-}
-
-__device__ __forceinline__ void coop_pick(float& bt, int& bk, float t2, int k2) {
-    if (t2 < bt || (t2 == bt && k2 > bk)) {
-        bt = t2;
-        bk = k2;
-    }
-}
-
-template <int CTRL>
-__device__ __forceinline__ void coop_step(float& bt, int& bk) {
-    const float t2 = __int_as_float(dpp_i<CTRL>(__float_as_int(bt)));
-    const int k2 = dpp_i<CTRL>(bk);
-    coop_pick(bt, bk, t2, k2);
-}
-
 // RT_KEY of a primitive id (spheres, planes, triangles, quads in turn); -1 for -1
 __device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
     const int e_pln = K.n_sph, e_tri = e_pln + K.n_pln, e_quad = e_tri + K.n_tri;
@@ -272,88 +241,6 @@ __device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
                   : id < e_pln ? RT_KEY(0, id)
                                : id < e_tri ? RT_KEY(1, id - e_pln)
                                             : id < e_quad ? RT_KEY(2, id - e_tri) : RT_KEY(3, id - e_quad);
-}
-
-template <bool QUADS>
-__device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_float* sc, f3 o, f3 d, int sl, int S,
-                                                 float& best_t, int& best_id) {
-    const float a = dot(d, d);
-    const float a4 = 4.0f * a;
-    const float a2 = 2.0f * a;
-    const CullRay cr = cull_ray(K, o, d, a);
-    const int e_pln = K.n_sph, e_tri = e_pln + K.n_pln, e_quad = e_tri + K.n_tri;
-    const int n = QUADS ? e_quad + K.n_quad : e_quad;
-    const lds_float* pln = sc + RT_SPH_FLOATS * K.n_sph;
-    const lds_float* tri = pln + RT_PLN_FLOATS * K.n_pln;
-    const lds_float* quad = tri + RT_TRI_FLOATS * K.n_tri;
-    float bt = INFINITY;
-    int bk = -1;
-    for (int j = sl; j < n; j += S) {
-        float t = INFINITY;
-        int key = -1;
-        if (j < e_pln) {  // sphere j, Intersection.cuh:15-62 (closest_hit_brute's test)
-            const v4f s = *reinterpret_cast<const lds_v4f*>(sc + RT_SPH_FLOATS * j);
-            const f3 xp = mk(o.x - s.x, o.y - s.y, o.z - s.z);
-            const float b = 2.0f * dot(xp, d);
-            const float c = dot(xp, xp) - s.w;
-            const float disc = b * b - a4 * c;
-            if (!(disc < 0.0f) && !(b >= 0.0f && disc == disc && a2 > 0.0f)) {
-                t = (-b - rt_sqrt(disc)) / a2;
-                key = RT_KEY(0, j);
-            }
-        } else if (j < e_tri) {  // plane, Intersection.cuh:64-106
-            const int i = j - e_pln;
-            const v4f q = *reinterpret_cast<const lds_v4f*>(pln + RT_PLN_FLOATS * i);
-            const float nd = q.x * d.x + q.y * d.y + q.z * d.z;
-            if (!(fabsf(nd) < RT_NEAR_ZERO)) {
-                t = -((q.x * o.x + q.y * o.y + q.z * o.z) + q.w) / nd;
-                key = RT_KEY(1, i);
-            }
-        } else {  // triangle / quad, Intersection.cuh:108-173 (polygon_test)
-            const bool is_tri = !QUADS || j < e_quad;
-            const int i = is_tri ? j - e_tri : j - e_quad;
-            const int nv = is_tri ? 3 : 4;
-            const lds_float* q = is_tri ? tri + RT_TRI_FLOATS * i : quad + RT_QUAD_FLOATS * i;
-            const v4f cs = *reinterpret_cast<const lds_v4f*>(q + (is_tri ? RT_TRI_CULL : RT_QUAD_CULL));
-            const float wx = cs.x - o.x, wy = cs.y - o.y, wz = cs.z - o.z;
-            const float ww = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
-            const float pj = __builtin_fmaf(wx, d.x, __builtin_fmaf(wy, d.y, wz * d.z));
-            const bool cull = cr.ok && __builtin_fmaf(-pj, pj, ww * cr.a_k) > cs.w * cr.a;
-            if (!cull) {
-                const v4f pl = *reinterpret_cast<const lds_v4f*>(q);
-                const float nd = pl.x * d.x + pl.y * d.y + pl.z * d.z;
-                if (!(fabsf(nd) < RT_NEAR_ZERO)) {
-                    const float tp = -((pl.x * o.x + pl.y * o.y + pl.z * o.z) + pl.w) / nd;
-                    const int kp = RT_KEY(is_tri ? 2 : 3, i);
-                    if (key_accept(tp, kp, bt, bk)) {
-                        const f3 P = add(o, scale(tp, d));
-                        bool inside = true;
-                        for (int k = 0; k < 4; k++) {
-                            if (k < nv) {
-                                const lds_float* e = q + RT_POLY_EDGES + 6 * k;
-                                if (dot(mk(e[3], e[4], e[5]), sub(P, mk(e[0], e[1], e[2]))) < 0.0f) inside = false;
-                            }
-                        }
-                        if (inside) {
-                            t = tp;
-                            key = kp;
-                        }
-                    }
-                }
-            }
-        }
-        if (key >= 0 && key_accept(t, key, bt, bk)) {
-            bt = t;
-            bk = key;
-        }
-    }
-    if (S >= 2) coop_step<0xB1>(bt, bk);   // quad_perm [1,0,3,2]
-    if (S >= 4) coop_step<0x4E>(bt, bk);   // quad_perm [2,3,0,1]
-    if (S >= 8) coop_step<0x141>(bt, bk);  // row_half_mirror
-    if (S >= 16) coop_step<0x140>(bt, bk); // row_mirror
-    best_t = bt;
-    const int kind = bk & 3, idx = bk >> 2;
-    best_id = bk < 0 ? -1 : idx + (kind == 0 ? 0 : kind == 1 ? e_pln : kind == 2 ? e_tri : e_quad);
 }
 
 }  // namespace
@@ -390,24 +277,6 @@ __device__ __forceinline__ void coop_closest_hit(const rt_kparams& K, const lds_
 // occupancy target of the pair kernel
 #ifndef RT_PAIR_WAVES
 #define RT_PAIR_WAVES 7
-#endif
-
-// spread launches of one owner wave: the executor wave takes half of every
-// closest hit (0 = off)
-#ifndef RT_SPLIT_HIT
-#define RT_SPLIT_HIT 1
-#endif
-// tail mode of the sorted kernel compiled in (K.tail_n turns it on per launch)
-#ifndef RT_TAIL
-#define RT_TAIL 1
-#endif
-// deferred fold (global-record kernels): a finished path's records are
-// folded by the executor of the pixel's next front task (its camera ray, or
-// a fold-only task after its last frame) instead of by the owner lane in the
-// I-phase, where only the lanes whose path just ended run it (9.3 of 64
-// lanes per instruction, profiles/r04/check_a/phase_lanes.json)
-#ifndef RT_DEFER_FOLD
-#define RT_DEFER_FOLD 0  // off: measured slower (c3 0.79 vs 0.75 ms, c4 5.81 vs 5.50)
 #endif
 
 template <int BLOCK, bool HIT_LDS, bool BVH>
@@ -668,275 +537,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 
 
 
-// specular_scatter (rt_path.h, Main.cu:245-255) for a tail segment whose
-// lanes hold the same ray: the two sincos_nn of the microfacet sample and the
-// two G1 terms of specularWeight each run on partner lanes (sl even / odd,
-// exchanged with a DPP quad_perm [1,0,3,2]), so a lone path's SPEC task
-// carries one of each on its dependency chain.  Same operations, same
-// operands, same results (a float product is commutative).  Needs S >= 2.
-__device__ __forceinline__ f3 specular_scatter_pair(Xorwow& rs, f3 d, f3 n, float rough, float rough2, float ior2m1,
-                                                    float& kspec, int sl) {
-    const bool odd = sl & 1;
-    const float e1 = rand_range(rs, 1.0f);
-    const float e2 = rand_range(rs, 1.0f);
-    const float theta = atan_nn(rough * rt_sqrt(e1) / rt_sqrt(1.0f - e1));
-    const float phi = 2.0f * RT_PI * e2;
-    float s_, c_;
-    sincos_nn(odd ? phi : theta, s_, c_);
-    const float s2 = __int_as_float(dpp_i<0xB1>(__float_as_int(s_)));
-    const float c2 = __int_as_float(dpp_i<0xB1>(__float_as_int(c_)));
-    const float st = odd ? s2 : s_, ct = odd ? c2 : c_;  // theta's, from the even lane
-    const float sp = odd ? s_ : s2, cp = odd ? c_ : c2;  // phi's, from the odd lane
-    const f3 mloc = mk(st * cp, st * sp, ct);
-    f3 some = mk(1.0f, 0.0f, 0.0f);
-    if (fabsf(dot(n, some)) < 1.0f - RT_NEAR_ZERO) some = mk(0.0f, 1.0f, 0.0f);
-    const f3 t1 = cross(n, some);
-    const f3 t2 = cross(n, t1);
-    const f3 m = mk(dot(mk(t1.x, t2.x, n.x), mloc), dot(mk(t1.y, t2.y, n.y), mloc), dot(mk(t1.z, t2.z, n.z), mloc));
-    const f3 scatter = sub(d, scale(2.0f * dot(d, m), m));
-    const f3 inc = scale(-1.0f, d);
-    const float fr = fresnel(inc, m, ior2m1);
-    // specular_weight(inc, scatter, n, m, rough2): G1(inc) on the even lane,
-    // G1(scatter) on the odd one
-    const float g1 = shadowing_masking(odd ? scatter : inc, n, m, rough2);
-    const float g1p = __int_as_float(dpp_i<0xB1>(__float_as_int(g1)));
-    float g = g1 * g1p;
-    float sw;
-    if (isnan(g)) {
-        sw = 1.0f;
-    } else {
-        float den = fabsf(dot(inc, n) * dot(m, n));
-        if (den == 0.0f) den = RT_NEAR_ZERO;
-        sw = fabsf(dot(inc, m)) * g / den;
-    }
-    kspec = sw * fr / RT_SPECULAR_CHANCE;
-    return scatter;
-}
-
-// Tail mode of rt_render_sorted_kernel (see there): a wave finishes its own
-// last `live` pixels from their hand-off records H; segments of S lanes per
-// pixel run its tasks redundantly and split its closest hits
-// (coop_closest_hit).  Not inlined (see the call).
 enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };  // a lane's next task
-// deferred fold (RT_DEFER_FOLD): the lane's finished path waits to be folded
-// by its next front task (T_REGEN | T_FOLD, or T_FOLD alone after the last frame)
-enum { T_FOLD = 8 };
-template <int BLOCK, bool HIT_LDS, bool GREC, bool QUADS>
-__device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((address_space(4))) rt_kparams* kp_arg,
-                                                      int tail_live_arg) {
-    // everything uniform comes from the kernel-argument segment and the LDS
-    // base.  The arguments of a call arrive in VGPRs, so the pointer is made
-    // wave-uniform here (scalar loads of the scene and the parameters instead
-    // of per-lane vector loads; the hit table from LDS, not through flat
-    // loads).  The kernarg-segment intrinsic itself is valid in kernels only:
-    // in a callee it yields a null base
-    extern __shared__ float smem[];
-    const unsigned long long kpi = (unsigned long long)kp_arg;
-    const unsigned kp_lo = __builtin_amdgcn_readfirstlane((unsigned)kpi);
-    const unsigned kp_hi = __builtin_amdgcn_readfirstlane((unsigned)(kpi >> 32));
-    const __attribute__((address_space(4))) rt_kparams* kp =
-        (const __attribute__((address_space(4))) rt_kparams*)(((unsigned long long)kp_hi << 32) | kp_lo);
-    const rt_kparams& K = *(const rt_kparams*)kp;
-    const int tail_live = __builtin_amdgcn_readfirstlane(tail_live_arg);  // this wave's live pixels
-    const int tid = threadIdx.x & 63;
-    const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
-    const float* hit_tab = HIT_LDS ? smem : K.hit;
-    float* rec_base = HIT_LDS ? smem + ((n_prim * RT_HIT_FLOATS + 3) & ~3) : smem;
-    const int levels = K.max_bounces;
-    const int LL = GREC ? (levels < RT_GREC_LDS_LEVELS ? levels : RT_GREC_LDS_LEVELS) : levels;
-    const lds_float* slots = (const lds_float*)(rec_base + 3 * LL * BLOCK);
-    const lds_float* H = slots + (threadIdx.x >> 6) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
-    const lds_float* sc = slots + (BLOCK / 64) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
-    const long npix = (long)K.rows * K.width;
-    const int GL = K.max_bounces - LL;
-    const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
-    const f3 o = mk(0.0f, 0.0f, 0.0f), d = o, hn = o;
-    // segment size: 64 / (live pixels rounded up to a power of 2), at most 16
-    const int p2 = tail_live <= 1 ? 1 : 1 << (32 - __builtin_clz(tail_live - 1));
-#ifndef RT_TAIL_COOP  // A/B builds: 0 = one lane per pixel (the barrier-free loop alone)
-#define RT_TAIL_COOP 1
-#endif
-    const int S = !RT_TAIL_COOP ? 1 : 64 / p2 < 16 ? 64 / p2 : 16;
-    const int seg = tid / S, sl = tid - seg * S;
-    bool live = seg < tail_live;
-    PixelState q;
-    int tmode = T_NONE, otid = 0;
-    f3 to = o, td = d, thn = hn;
-    int thid = 0, tdepth = 0;
-    if (live) {
-#define HR(f) H[(f) * RT_TAIL_MAX + seg]
-        q.p = __float_as_int(HR(0));
-        q.frame = __float_as_uint(HR(1));
-        q.passes_left = __float_as_int(HR(2));
-        q.ax = HR(3);
-        q.ay = HR(4);
-        q.az = HR(5);
-        q.d0 = mk(HR(6), HR(7), HR(8));
-        q.rs.d = __float_as_uint(HR(9));
-        q.rs.v0 = __float_as_uint(HR(10));
-        q.rs.v1 = __float_as_uint(HR(11));
-        q.rs.v2 = __float_as_uint(HR(12));
-        q.rs.v3 = __float_as_uint(HR(13));
-        q.rs.v4 = __float_as_uint(HR(14));
-        to = mk(HR(15), HR(16), HR(17));
-        td = mk(HR(18), HR(19), HR(20));
-        thn = mk(HR(21), HR(22), HR(23));
-        thid = __float_as_int(HR(24));
-        tdepth = __float_as_int(HR(25));
-        tmode = __float_as_int(HR(26));
-        otid = __float_as_int(HR(27));
-#undef HR
-    }
-    lds_float* trec = (lds_float*)(rec_base + otid);
-    constexpr bool DF = GREC && RT_DEFER_FOLD;  // (the kernel's deferred fold: its record layout)
-    const int GLD = DF ? GL + 1 : GL;
-    float* tgrec = GREC ? K.rec + (long)blockIdx.x * 3 * GLD * BLOCK + otid : rec_base;
-    if (DF && live && (tmode & T_FOLD)) {  // a finished path handed over unfolded
-        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];
-        if (tdepth > K.max_bounces) {
-            const float* r = tgrec + 3 * GL * BLOCK;
-            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
-        }
-        const int nrec = tdepth > K.max_bounces ? K.max_bounces : tdepth;
-        for (int l = nrec - 1; l >= LL; --l) {
-            const float* r = tgrec + 3 * (l - LL) * BLOCK;
-            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
-        }
-        for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-            const lds_float* r = trec + 3 * l * BLOCK;
-            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
-        }
-        if (q.frame == 1u) {
-            q.ax = 0.0f;
-            q.ay = 0.0f;
-            q.az = 0.0f;
-        }
-        q.ax = q.ax + lx;
-        q.ay = q.ay + ly;
-        q.az = q.az + lz;
-        q.frame++;
-        q.passes_left--;
-        tmode &= 7;  // T_REGEN, or T_NONE after the last frame
-        if (tmode == T_NONE) {
-            store_pixel(K, npix, q);
-            live = false;
-        }
-    }
-#ifdef RT_STAMPS
-    // diagnostic: K.stamps[32] tail wave-cycles, [33] tail rounds, [34]
-    // tail entries, [35] pixels handed over
-    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
-    unsigned long long st_rounds = 0;
-#endif
-    while (__any(live)) {
-#ifdef RT_STAMPS
-        st_rounds++;
-#endif
-        bool has_ray = false, tended = false;
-        int lcode = 0;
-        float lk = 0.0f, lc = 0.0f;
-        // the task of the round (T-phase): camera ray or bounce direction
-        if (live) {
-            if (tmode == T_REGEN) {  // Main.cu:290-292
-                const f3 r = random_direction(q.rs, q.d0);
-                td = normalize3(add(q.d0, scale(K.jitter, r)));
-                to = cam;
-                tdepth = 0;
-                has_ray = true;
-            } else {
-                float kspec = 0.0f;
-                int code = thid;
-                if (tmode == T_SPEC) {  // Main.cu:245-255
-                    const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * thid + 8);
-                    if (RT_TAIL_COOP)
-                        td = specular_scatter_pair(q.rs, td, thn, h2.x, h2.z, h2.y, kspec, sl);  // S >= 4 here
-                    else
-                        td = specular_scatter(q.rs, td, thn, h2.x, h2.z, h2.y, kspec);
-                    code = ~thid;
-                } else {  // diffuse, Main.cu:257-260
-                    td = random_direction(q.rs, thn);
-                }
-                const float cosang = dot(td, thn);  // cosAngle, Main.cu:264
-                if (tdepth < K.max_bounces) {
-                    if (!GREC || tdepth < LL) {
-                        lds_float* r = trec + 3 * tdepth * BLOCK;
-                        r[0] = __int_as_float(code);
-                        r[BLOCK] = kspec;
-                        r[2 * BLOCK] = cosang;
-                    } else {
-                        float* r = tgrec + 3 * (tdepth - LL) * BLOCK;
-                        r[0] = __int_as_float(code);
-                        r[BLOCK] = kspec;
-                        r[2 * BLOCK] = cosang;
-                    }
-                    has_ray = true;
-                } else {  // the deepest level (Main.cu:210): kept in registers
-                    lcode = code;
-                    lk = kspec;
-                    lc = cosang;
-                    tended = true;
-                }
-                tdepth++;
-            }
-        }
-        // closest hit (Main.cu:214-234), split over the segment
-        float t = INFINITY;
-        int id = -1;
-        if (has_ray) {
-            if (RT_TAIL_COOP && bvh_safe(K, to, td))
-                coop_closest_hit<QUADS>(K, sc, to, td, sl, S, t, id);
-            else  // NaN-capable tests: the reference's own loop order
-                closest_hit_brute<QUADS>(K, to, td, t, id);
-            if (id >= 0) {
-                const float4 h0 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * id);
-                to = add(to, scale(t, td));
-                thn = mk(h0.x, h0.y, h0.z);
-                if (h0.w != 0.0f) thn = normalize3(sub(to, thn));
-                thid = id;
-                tmode = rand_range(q.rs, 1.0f) < RT_SPECULAR_CHANCE ? T_SPEC : T_DIFF;  // Main.cu:243
-            } else {
-                tended = true;
-            }
-        }
-        if (tended) {  // fold, accumulate (Main.cu:262-268, 299-304)
-            float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];
-            if (tdepth > K.max_bounces) fold_level(lcode, lk, lc, hit_tab, lx, ly, lz);
-            const int nrec = tdepth > K.max_bounces ? K.max_bounces : tdepth;
-            if (GREC)
-                for (int l = nrec - 1; l >= LL; --l) {
-                    const float* r = tgrec + 3 * (l - LL) * BLOCK;
-                    fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
-                }
-            for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-                const lds_float* r = trec + 3 * l * BLOCK;
-                fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
-            }
-            if (q.frame == 1u) {
-                q.ax = 0.0f;
-                q.ay = 0.0f;
-                q.az = 0.0f;
-            }
-            q.ax = q.ax + lx;
-            q.ay = q.ay + ly;
-            q.az = q.az + lz;
-            q.frame++;
-            q.passes_left--;
-            tmode = q.passes_left > 0 ? T_REGEN : T_NONE;
-            if (tmode == T_NONE) {  // pixel done (every lane of the segment stores the same words)
-                store_pixel(K, npix, q);
-                live = false;
-            }
-        }
-    }
-#ifdef RT_STAMPS
-    if (tid == 0 && K.stamps) {
-        atomicAdd(&K.stamps[32], __builtin_amdgcn_s_memtime() - st_t0);
-        atomicAdd(&K.stamps[33], st_rounds);
-        atomicAdd(&K.stamps[34], 1ull);
-        atomicAdd(&K.stamps[35], (unsigned long long)tail_live);
-    }
-#endif
-}
 
 // ===========================================================================
 // Sorted task-queue megakernel (the product path).
@@ -959,23 +560,13 @@ __device__ __attribute__((noinline)) void rt_tail_run(const __attribute__((addre
 //            miss (or the depth limit) folds the path's records, accumulates
 //            the frame and schedules the pixel's next camera ray.
 //
-// LDS: [hit table][record stack 3 x (max_bounces+1) x BLOCK]
+// LDS: [hit table][record stack 3 x levels x BLOCK]
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
-// TAIL: the tail-mode instantiation (launched only when K.tail_n > 0: its
-// code costs the main loop spilled SGPRs even when no group enters it)
-// OWN: pixels per workgroup (lanes 0 .. OWN-1 own one each; the others only
-// execute tasks).  OWN = BLOCK / 2 ("spread", small shards): a round's tasks
-// never fill more than half the queue, so the RANDDIR tasks (front) and the
-// SPEC tasks (back) land in different waves instead of one wave running both
-template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER = false, bool QUADS = true, bool TAIL = false,
-          int OWN = BLOCK>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(!BVH && (GREC || TAIL) ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
+// GREC: the record levels >= RT_GREC_LDS_LEVELS in global memory (deep paths
+// and full frames, launch policy).  BVH scenes take the ray-refill kernel.
+template <int BLOCK, bool HIT_LDS, bool GREC, bool ORDER = false, bool QUADS = true>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
-    static_assert(OWN == BLOCK || (!TAIL && OWN % 64 == 0 && OWN < BLOCK), "spread launches: no tail mode");
-    constexpr int RS = OWN;  // record-stack stride: one column per owner lane
-    // split closest hits: one owner wave (its take-back reads and the ray
-    // posts are ordered within the wave) and one executor wave
-    constexpr bool SPLIT = !BVH && OWN == 64 && BLOCK == 128 && RT_SPLIT_HIT;
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1002,21 +593,13 @@ rt_render_sorted_kernel(rt_kparams K) {
     // base held across the loop)
     lds_float* rec = (lds_float*)(rec_base + tid);
     const int GL = levels - LL;
-    // deferred fold: the deepest level (max_bounces) goes to global memory
-    // too, as level GL, so it outlives the round that made it
-    constexpr bool DF = GREC && !BVH && RT_DEFER_FOLD;
-    const int GLD = DF ? GL + 1 : GL;
-    float* grec = GREC ? K.rec + (long)blockIdx.x * 3 * GLD * RS + tid : rec_base;
-    float* slots = rec_base + 3 * LL * RS;
+    float* grec = GREC ? K.rec + (long)blockIdx.x * 3 * GL * BLOCK + tid : rec_base;
+    float* slots = rec_base + 3 * LL * BLOCK;
     int* counters = reinterpret_cast<int*>(slots + 13 * BLOCK);
     // counters[0..3]: queue fronts/backs (2 parities)
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
     if (tid < 4) counters[tid] = 0;
-    // counters[4]: the tail threshold, read with the queue counters each
-    // round (from the kernel arguments it is an extra scalar load and wait
-    // per round: the loop's SGPRs do not keep it)
-    if (TAIL && tid == 4) counters[4] = K.tail_n;
 #ifdef RT_GTIMES
     // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g], [2g+1]
     if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1035,7 +618,10 @@ rt_render_sorted_kernel(rt_kparams K) {
     const long group = ORDER && K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
     if (ORDER && tid == 0) K.group_cost[group] = (unsigned)__builtin_amdgcn_s_memrealtime();
     PixelState px;
-    load_item(K, npix, nitems, tid < OWN ? group * OWN + tid : nitems, px);  // (lanes >= OWN: no pixel)
+    // (tid < BLOCK always holds; the guard keeps the register allocation and
+    // schedule of the measured kernel: without it the instruction stream
+    // differs in 55 places, `make asm`)
+    load_item(K, npix, nitems, tid < BLOCK ? group * BLOCK + tid : nitems, px);
     int mode = px.passes_left > 0 ? T_REGEN : T_NONE;
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -1053,12 +639,12 @@ rt_render_sorted_kernel(rt_kparams K) {
         const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
         if (GREC)
             for (int l = nrec - 1; l >= LL; --l) {
-                const float* r = grec + 3 * (l - LL) * RS;
-                fold_level(__float_as_int(r[0]), r[RS], r[2 * RS], hit_tab, lx, ly, lz);
+                const float* r = grec + 3 * (l - LL) * BLOCK;
+                fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
             }
         for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-            const lds_float* r = rec + 3 * l * RS;
-            fold_level(__float_as_int(r[0]), r[RS], r[2 * RS], hit_tab, lx, ly, lz);
+            const lds_float* r = rec + 3 * l * BLOCK;
+            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
         }
 #if RT_PHASE_TWICE == 4
         {
@@ -1067,12 +653,12 @@ rt_render_sorted_kernel(rt_kparams K) {
                 fold_level(__float_as_int(opq(SLOT(6, slot))), opq(SLOT(4, slot)), opq(SLOT(5, slot)), hit_tab, mx, my, mz);
             if (GREC)
                 for (int l = nrec - 1; l >= LL; --l) {
-                    const float* r = grec + 3 * (l - LL) * RS;
-                    fold_level(__float_as_int(opq(r[0])), opq(r[RS]), opq(r[2 * RS]), hit_tab, mx, my, mz);
+                    const float* r = grec + 3 * (l - LL) * BLOCK;
+                    fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
                 }
             for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-                const lds_float* r = rec + 3 * l * RS;
-                fold_level(__float_as_int(opq(r[0])), opq(r[RS]), opq(r[2 * RS]), hit_tab, mx, my, mz);
+                const lds_float* r = rec + 3 * l * BLOCK;
+                fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
             }
             keep(mx + my + mz);
         }
@@ -1093,9 +679,6 @@ rt_render_sorted_kernel(rt_kparams K) {
         mode = px.passes_left > 0 ? T_REGEN : T_NONE;
     };
     bool ended = false;  // path ended this round: finish_path() once, after the I-phase
-    // tail mode (below the loop): live pixels of the group and this lane's
-    // hand-off index (-1: no live pixel)
-    int tail_live = 0, tail_c = -1;
 
 #ifdef RT_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1134,8 +717,7 @@ rt_render_sorted_kernel(rt_kparams K) {
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
         int* cnt = counters + 2 * parity;
-        // (deferred fold: T_REGEN | T_FOLD and T_FOLD alone are front tasks)
-        const bool front = DF ? ((task & 7) == T_REGEN || task == T_DIFF || task == T_FOLD) : task == T_REGEN || task == T_DIFF;
+        const bool front = task == T_REGEN || task == T_DIFF;
         const unsigned long long mf = __ballot(front);
         const unsigned long long mbk = __ballot(task == T_SPEC);
         int base_f = 0, base_b = 0;
@@ -1149,18 +731,15 @@ rt_render_sorted_kernel(rt_kparams K) {
         if (front) slot = base_f + lanes_below(mf);
         if (task == T_SPEC) slot = BLOCK - 1 - (base_b + lanes_below(mbk));
         if (slot >= 0) {
-            const f3 nrm = (DF ? (task & 7) == T_REGEN : task == T_REGEN) ? px.d0 : hn;
+            const f3 nrm = task == T_REGEN ? px.d0 : hn;
             SLOT(0, slot) = nrm.x;
             SLOT(1, slot) = nrm.y;
             SLOT(2, slot) = nrm.z;
             SLOT(3, slot) = d.x;
             SLOT(4, slot) = d.y;
             SLOT(5, slot) = d.z;
-            // code: primitive id (bounce), -1 (camera ray), or for a deferred
-            // fold -(2 + depth + 64 tid [+ 2^20 when no camera ray follows])
-            int code = task == T_REGEN ? -1 : hid;
-            if (DF && (task & T_FOLD)) code = -(2 + depth + 64 * tid + (task == T_FOLD ? (1 << 20) : 0));
-            SLOT(6, slot) = __int_as_float(code);
+            // code: primitive id (bounce) or -1 (camera ray)
+            SLOT(6, slot) = __int_as_float(task == T_REGEN ? -1 : hid);
             SLOT(7, slot) = __uint_as_float(px.rs.d);
             SLOT(8, slot) = __uint_as_float(px.rs.v0);
             SLOT(9, slot) = __uint_as_float(px.rs.v1);
@@ -1174,18 +753,7 @@ rt_render_sorted_kernel(rt_kparams K) {
         // no task anywhere in the workgroup: every lane is idle (rays are
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
-        int tail_thr = 0;
-        if (TAIL) {
-            tail_thr = counters[4];
-            asm volatile("" ::"v"(tail_thr));  // read together with the counters (one LDS wait)
-        }
         if (nf + nb == 0) break;
-        // few live pixels left (one per posted task; group-uniform): each
-        // wave finishes its own in the tail loop below instead of this round
-        if (TAIL && !BVH && nf + nb <= tail_thr) {
-            tail_live = nf + nb;
-            break;
-        }
 
         // ---- T-phase: execute slot `tid`
         {
@@ -1225,38 +793,8 @@ rt_render_sorted_kernel(rt_kparams K) {
                         keep_i((int)r2.v4);
                     }
 #endif
-                    const bool fold = DF && code < -1;  // a finished path to fold
-                    const int fv = -code - 2;           // (fold) depth | tid << 6 | fold-only << 20
-                    r = nrm;
-                    if (!fold || !(fv >> 20)) {
-                        r = random_direction(rs, nrm, rej_ptr);
-                        if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
-                    }
-                    if (fold) {
-                        // the owner's finished path, innermost-first (Main.cu:262-268),
-                        // from its record stack: level max_bounces and the deep
-                        // levels in global memory, the shallow ones in LDS
-                        const int od = fv & 63, ot = (fv >> 6) & 1023;
-                        const float* gq = K.rec + (long)blockIdx.x * 3 * GLD * RS + ot;
-                        const lds_float* lq = (const lds_float*)(rec_base + ot);
-                        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
-                        if (od > K.max_bounces) {
-                            const float* q = gq + 3 * GL * RS;
-                            fold_level(__float_as_int(q[0]), q[RS], q[2 * RS], hit_tab, lx, ly, lz);
-                        }
-                        const int nrec = od > K.max_bounces ? K.max_bounces : od;
-                        for (int l = nrec - 1; l >= LL; --l) {
-                            const float* q = gq + 3 * (l - LL) * RS;
-                            fold_level(__float_as_int(q[0]), q[RS], q[2 * RS], hit_tab, lx, ly, lz);
-                        }
-                        for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-                            const lds_float* q = lq + 3 * l * RS;
-                            fold_level(__float_as_int(q[0]), q[RS], q[2 * RS], hit_tab, lx, ly, lz);
-                        }
-                        SLOT(4, tid) = lx;  // (slot fields 4..6 are free once read)
-                        SLOT(5, tid) = ly;
-                        SLOT(6, tid) = lz;
-                    }
+                    r = random_direction(rs, nrm, rej_ptr);
+                    if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
                 } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
@@ -1324,53 +862,31 @@ rt_render_sorted_kernel(rt_kparams K) {
             px.rs.v3 = __float_as_uint(RES(8, slot));
             px.rs.v4 = __float_as_uint(RES(9, slot));
             mode = T_NONE;
-            if (DF ? (task & 7) == T_REGEN || task == T_FOLD : task == T_REGEN) {
-                if (DF && (task & T_FOLD)) {  // the finished path, folded by the executor
-                    const float lx = SLOT(4, slot), ly = SLOT(5, slot), lz = SLOT(6, slot);
-                    if (px.frame == 1u) {  // progressive accumulation (Main.cu:299-304)
-                        px.ax = 0.0f;
-                        px.ay = 0.0f;
-                        px.az = 0.0f;
-                    }
-                    px.ax = px.ax + lx;
-                    px.ay = px.ay + ly;
-                    px.az = px.az + lz;
-                    px.frame++;
-                    px.passes_left--;
-                }
-                if (task != T_FOLD) {
-                    o = cam;
-                    depth = 0;
-                    has_ray = true;
-                }
+            if (task == T_REGEN) {
+                o = cam;
+                depth = 0;
+                has_ray = true;
             } else {
                 const int code = task == T_SPEC ? ~hid : hid;
                 const float kspec = task == T_SPEC ? RES(3, slot) : 0.0f;
                 const float cosang = dot(d, hn);  // cosAngle, Main.cu:264
                 if (depth < K.max_bounces) {
                     if (!GREC || depth < LL) {  // (separate stores: LDS and global address spaces)
-                        lds_float* r = rec + 3 * depth * RS;
+                        lds_float* r = rec + 3 * depth * BLOCK;
                         r[0] = __int_as_float(code);
-                        r[RS] = kspec;
-                        r[2 * RS] = cosang;
+                        r[BLOCK] = kspec;
+                        r[2 * BLOCK] = cosang;
                     } else {
-                        float* r = grec + 3 * (depth - LL) * RS;
+                        float* r = grec + 3 * (depth - LL) * BLOCK;
                         r[0] = __int_as_float(code);
-                        r[RS] = kspec;
-                        r[2 * RS] = cosang;
+                        r[BLOCK] = kspec;
+                        r[2 * BLOCK] = cosang;
                     }
                     has_ray = true;  // from the hit point o along d
                 } else {  // next query would exceed maxBounces (Main.cu:210): the path ends
-                    if (DF) {  // the deepest level: global level GL, folded next round
-                        float* r = grec + 3 * GL * RS;
-                        r[0] = __int_as_float(code);
-                        r[RS] = kspec;
-                        r[2 * RS] = cosang;
-                    } else {
-                        SLOT(4, slot) = kspec;
-                        SLOT(5, slot) = cosang;
-                        SLOT(6, slot) = __int_as_float(code);
-                    }
+                    SLOT(4, slot) = kspec;
+                    SLOT(5, slot) = cosang;
+                    SLOT(6, slot) = __int_as_float(code);
                     ended = true;
                 }
                 depth++;
@@ -1388,66 +904,19 @@ rt_render_sorted_kernel(rt_kparams K) {
         }
 #endif
         // ---- I-phase: closest hit + brdfChoice (Main.cu:214-245)
-        // SPLIT (spread groups of one owner wave and one executor wave): the
-        // executor wave, idle here, takes half of every closest hit — the
-        // owner posts its ray in its own slot index (fields 0..3 and 7..12
-        // are free once the owner wave has taken its results back; 4..6 may
-        // hold a path's deepest level), each half tests every other index
-        // i of the reference's interleaved loop, and the owner keeps the
-        // smaller distance, ties to the larger key (the reference's result
-        // for rays that pass bvh_safe; the others take the whole loop)
-        bool split = false;
         float t = INFINITY;
         int id = -1;
-        if constexpr (SPLIT) {
-            if (tid < OWN) {
-                split = has_ray && bvh_safe(K, o, d);
-                SLOT(0, tid) = o.x;
-                SLOT(1, tid) = o.y;
-                SLOT(2, tid) = o.z;
-                SLOT(3, tid) = d.x;
-                SLOT(7, tid) = d.y;
-                SLOT(8, tid) = d.z;
-                SLOT(9, tid) = __int_as_float(split ? 1 : 0);
-            }
-            __syncthreads();
-            if (tid >= OWN) {
-                const int ot = tid - OWN;
-                if (__float_as_int(SLOT(9, ot))) {
-                    float t2;
-                    int id2;
-                    closest_hit_brute<QUADS, 2>(K, mk(SLOT(0, ot), SLOT(1, ot), SLOT(2, ot)),
-                                                mk(SLOT(3, ot), SLOT(7, ot), SLOT(8, ot)), t2, id2, 1);
-                    SLOT(10, ot) = t2;
-                    SLOT(11, ot) = __int_as_float(id2);
-                }
-            }
-        }
         if (has_ray) {
 #if RT_PHASE_TWICE == 1
             {
                 float t2;
                 int id2;
-                closest_hit<BVH, QUADS>(K, opq3(o), opq3(d), t2, id2);
+                closest_hit_brute<QUADS>(K, opq3(o), opq3(d), t2, id2);
                 keep(t2);
                 keep_i(id2);
             }
 #endif
-            if (SPLIT && split)
-                closest_hit_brute<QUADS, 2>(K, o, d, t, id, 0);
-            else
-                closest_hit<BVH, QUADS>(K, o, d, t, id);
-        }
-        if constexpr (SPLIT) {
-            __syncthreads();
-            if (split) {  // the other half: smaller distance, ties to the larger key
-                const float t2 = SLOT(10, tid);
-                const int id2 = __float_as_int(SLOT(11, tid));
-                if (id2 >= 0 && (t2 < t || (t2 == t && prim_key(K, id2) > prim_key(K, id)))) {
-                    t = t2;
-                    id = id2;
-                }
-            }
+            closest_hit_brute<QUADS>(K, o, d, t, id);
         }
         if (has_ray) {
             has_ray = false;
@@ -1465,77 +934,11 @@ rt_render_sorted_kernel(rt_kparams K) {
         }
         if (ended) {
             ended = false;
-            if (DF)  // folded by the pixel's next front task: its camera ray, or a fold-only task
-                mode = (px.passes_left > 1 ? T_REGEN : T_NONE) | T_FOLD;
-            else
-                finish_path(slot);
+            finish_path(slot);
         }
         STAMP(6);
     }
     if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
-#if RT_TAIL
-    if (TAIL && !BVH && tail_live > 0) {  // group-uniform
-        // ---- tail mode.  The group's few live pixels (each with its task of
-        // this round still to run) leave the round loop: every wave finishes
-        // its own in a loop without barriers or task slots, each pixel held
-        // by a segment of S lanes that run its tasks redundantly (the same
-        // RNG stream, the same results) and split its closest hits.  The
-        // hand-off records [field][pixel] go to the task-slot area (free:
-        // this round's slots are never executed), one per wave, the scene's
-        // records behind them (the launcher checks that all fit).
-        // every wave keeps its own live pixels: wave w's hand-off record at
-        // slots + w * RT_TAIL_FIELDS * RT_TAIL_MAX, index = live lanes below
-        const unsigned long long live_mask = __ballot(mode != T_NONE);
-        if (mode != T_NONE) tail_c = lanes_below(live_mask);
-        lds_float* H = (lds_float*)slots + (tid >> 6) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
-        lds_float* sc = (lds_float*)slots + (BLOCK / 64) * (RT_TAIL_FIELDS * RT_TAIL_MAX);
-        if (tail_c >= 0) {
-#define HW(f, v) H[(f) * RT_TAIL_MAX + tail_c] = (v)
-            HW(0, __int_as_float((int)px.p));
-            HW(1, __uint_as_float(px.frame));
-            HW(2, __int_as_float(px.passes_left));
-            HW(3, px.ax);
-            HW(4, px.ay);
-            HW(5, px.az);
-            HW(6, px.d0.x);
-            HW(7, px.d0.y);
-            HW(8, px.d0.z);
-            HW(9, __uint_as_float(px.rs.d));
-            HW(10, __uint_as_float(px.rs.v0));
-            HW(11, __uint_as_float(px.rs.v1));
-            HW(12, __uint_as_float(px.rs.v2));
-            HW(13, __uint_as_float(px.rs.v3));
-            HW(14, __uint_as_float(px.rs.v4));
-            HW(15, o.x);
-            HW(16, o.y);
-            HW(17, o.z);
-            HW(18, d.x);
-            HW(19, d.y);
-            HW(20, d.z);
-            HW(21, hn.x);
-            HW(22, hn.y);
-            HW(23, hn.z);
-            HW(24, __int_as_float(hid));
-            HW(25, __int_as_float(depth));
-            HW(26, __int_as_float(mode));
-            HW(27, __int_as_float(tid));
-#undef HW
-        }
-        const int nsc = RT_SPH_FLOATS * K.n_sph + RT_PLN_FLOATS * K.n_pln + RT_TRI_FLOATS * K.n_tri +
-                        (QUADS ? RT_QUAD_FLOATS * K.n_quad : 0);
-        for (int i = tid; i < nsc; i += BLOCK) sc[i] = K.sph[i];  // sph | pln | tri | quad are contiguous
-        __syncthreads();
-        if (live_mask) {  // (wave-uniform)
-            // a call, not inlined: the tail's registers stay out of the main
-            // loop's allocation (inlined, it cost the global-record kernel 6
-            // spilled VGPRs and 29 more spilled SGPRs)
-            rt_tail_run<BLOCK, HIT_LDS, GREC, QUADS>(
-                (const __attribute__((address_space(4))) rt_kparams*)__builtin_amdgcn_kernarg_segment_ptr(),
-                __popcll(live_mask));
-        }
-        __syncthreads();  // the group's span (ORDER, GTIMES) ends with its last wave
-    }
-#endif
     // the loop exit is group-uniform (the round that posts no task), so one
     // lane's clock after the loop closes the group's span
     if (ORDER && tid == 0) {
@@ -2160,37 +1563,44 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
 // tile-group costs into group_order (0 = none; the context resets it before
 // each launch and keeps the value as the order's grid)
 extern thread_local long rt_order_groups_last;
+// the render kernel the last launch on this thread took (rt_last_kernel_name)
+extern thread_local char rt_launched_kernel[96];
 hipError_t rt_launch_order_groups(const unsigned* cost, int* order, long n, hipStream_t stream);
 
 namespace {
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC, int OWN = BLOCK, bool PAIR = false>
+// render kernels: one path per lane (A/B reference, samplesPerPixel > 1),
+// the sorted task-queue kernel (full frames), the pair kernel (small frames
+// and shards: 128 lanes for 64 pixels)
+enum { K_SIMPLE = 0, K_SORTED = 1, K_PAIR = 2 };
+
+template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, bool GREC = false, bool ORDER = false, bool QUADS = true>
 void* kernel_ptr() {
-    if constexpr (PAIR) return reinterpret_cast<void*>(&rt_render_pair_kernel<HIT_LDS, false, true>);
-    return SORTED ? reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, false, true, false, OWN>)
-                  : reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
+    if constexpr (KIND == K_PAIR) return reinterpret_cast<void*>(&rt_render_pair_kernel<HIT_LDS, ORDER, QUADS>);
+    if constexpr (KIND == K_SORTED)
+        return reinterpret_cast<void*>(&rt_render_sorted_kernel<BLOCK, HIT_LDS, GREC, ORDER, QUADS>);
+    return reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
 }
 
-template <int BLOCK, bool HIT_LDS, bool BVH, bool GREC, bool ORDER, bool QUADS, bool TAIL, int OWN, bool PAIR = false>
-void launch_sorted(const rt_kparams& K, long grid, size_t lds, hipStream_t stream) {
-    if constexpr (PAIR)
+template <int KIND, int BLOCK, bool HIT_LDS, bool GREC, bool ORDER, bool QUADS>
+void launch_kind(const rt_kparams& K, long grid, size_t lds, hipStream_t stream) {
+    if constexpr (KIND == K_PAIR)
         hipLaunchKernelGGL((rt_render_pair_kernel<HIT_LDS, ORDER, QUADS>), dim3((unsigned)grid), dim3(128), lds, stream, K);
     else
-        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, BVH, GREC, ORDER, QUADS, TAIL, OWN>),
-                           dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+        hipLaunchKernelGGL((rt_render_sorted_kernel<BLOCK, HIT_LDS, GREC, ORDER, QUADS>), dim3((unsigned)grid),
+                           dim3(BLOCK), lds, stream, K);
 }
 
-// OWN < BLOCK (sorted only): spread launch, OWN pixels per BLOCK-lane group;
-// PAIR: the pair kernel (128 lanes, 64 pixels) instead of the sorted one
-template <int BLOCK, bool HIT_LDS, bool SORTED, bool BVH, bool GREC = false, int OWN = BLOCK, bool PAIR = false>
+template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, bool GREC = false>
 hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
-    static_assert(!PAIR || (BLOCK == 128 && OWN == 64 && SORTED && !BVH && !GREC), "pair launches: 128 lanes, 64 pixels");
-    static_assert(OWN == BLOCK || SORTED, "spread launches: sorted kernel only");
+    static_assert(KIND != K_PAIR || (BLOCK == 128 && HIT_LDS && !BVH && !GREC), "pair launches: 128 lanes, 64 pixels");
+    static_assert(KIND == K_SIMPLE || !BVH, "BVH scenes: the ray-refill kernel");
+    constexpr int OWN = KIND == K_PAIR ? 64 : BLOCK;  // pixels per workgroup
     rt_kparams K = K0;
     const long nitems = launch_items(K);
     long grid = (nitems + OWN - 1) / OWN;  // streaming needs a resident grid only
-    if (grid_mult > 0 && !SORTED) {  // persistent (simple kernel): grid_mult x resident groups per CU x CUs
+    if (grid_mult > 0 && KIND == K_SIMPLE) {  // persistent (simple kernel): grid_mult x resident groups per CU x CUs
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC>(), BLOCK, lds) ==
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<KIND, BLOCK, HIT_LDS, BVH>(), BLOCK, lds) ==
                 hipSuccess &&
             per_cu > 0) {
             const long cap = (long)per_cu * num_cus * grid_mult;
@@ -2199,34 +1609,24 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     if (grid < 1) grid = 1;
     K.rec_stride = (int)(grid * OWN);
-    // tail mode: brute-force scenes whose compiled records fit in the task-slot
-    // area beside the hand-off record
-    if (K.tail_n > 0) {
-        const long nsc = (long)RT_SPH_FLOATS * K.n_sph + (long)RT_PLN_FLOATS * K.n_pln +
-                         (long)RT_TRI_FLOATS * K.n_tri + (long)RT_QUAD_FLOATS * K.n_quad;
-        if (!SORTED || BVH || !RT_TAIL || OWN != BLOCK || (long)(BLOCK / 64) * RT_TAIL_FIELDS * RT_TAIL_MAX + nsc > 13L * BLOCK)
-            K.tail_n = 0;
-        if (K.tail_n > RT_TAIL_MAX) K.tail_n = RT_TAIL_MAX;
-    }
-    // launch-order feedback: only where the sorted grid covers every item
-    // once (group g <-> tile-group g) and the buffers hold the grid
-    // and only where the grid runs in more than RT_ORDER_MIN_GEN generations
-    // of resident groups: LPT order shortens the drain at the end of a
+    // launch-order feedback: only where the grid covers every item once
+    // (group g <-> tile-group g) and the buffers hold the grid, and only
+    // where the grid runs in more than RT_ORDER_MIN_GEN generations of
+    // resident groups: LPT order shortens the drain at the end of a
     // multi-generation grid, while a grid that is resident all at once only
     // gets its expensive groups packed onto the same CUs (c3 at 1/8: 0.264
     // vs 0.243 ms with the order; 1/2: 0.493 vs 0.522)
-    // (the tail-mode instantiation runs without launch-order feedback)
-    bool feedback = SORTED && K.tail_n == 0 && K.group_cost && K.group_order && grid <= K.order_cap;
+    bool feedback = KIND != K_SIMPLE && K.group_cost && K.group_order && grid <= K.order_cap;
     if (feedback) {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<BLOCK, HIT_LDS, SORTED, BVH, GREC, OWN, PAIR>(),
-                                                         BLOCK, lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel_ptr<KIND, BLOCK, HIT_LDS, BVH, GREC>(), BLOCK,
+                                                         lds) != hipSuccess ||
             per_cu <= 0)
             per_cu = 1;
         // (pair launches always: their grid is about one generation, and the
         // order still helped there: c3 1/8 0.212 -> 0.206 ms, 1/16 0.187 ->
         // 0.183, profiles/r04/spread/ab_pair.txt vs ab_prio.txt)
-        feedback = PAIR || (double)grid > RT_ORDER_MIN_GEN * (double)per_cu * num_cus;
+        feedback = KIND == K_PAIR || (double)grid > RT_ORDER_MIN_GEN * (double)per_cu * num_cus;
     }
     if (!feedback) {
         K.group_cost = nullptr;
@@ -2236,27 +1636,22 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     // brute-force scenes without quads: the quad tests compiled out
     const bool quads = BVH || K.n_quad > 0;
-    if constexpr (SORTED) {
-        if constexpr (!BVH && RT_TAIL && OWN == BLOCK) {
-            if (K.tail_n > 0) {
-                if (quads)
-                    launch_sorted<BLOCK, HIT_LDS, false, GREC, false, true, true, OWN>(K, grid, lds, stream);
-                else
-                    launch_sorted<BLOCK, HIT_LDS, false, GREC, false, false, true, OWN>(K, grid, lds, stream);
-                return hipGetLastError();  // (no launch-order feedback with the tail)
-            }
-        }
-        if (feedback && quads)
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, true, false, OWN, PAIR>(K, grid, lds, stream);
-        else if (feedback)
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, true, false, false, OWN, PAIR>(K, grid, lds, stream);
-        else if (quads)
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, true, false, OWN, PAIR>(K, grid, lds, stream);
-        else
-            launch_sorted<BLOCK, HIT_LDS, BVH, GREC, false, false, false, OWN, PAIR>(K, grid, lds, stream);
-    } else {
+    if constexpr (KIND == K_SIMPLE) {
         hipLaunchKernelGGL((rt_render_kernel<BLOCK, HIT_LDS, BVH>), dim3((unsigned)grid), dim3(BLOCK), lds, stream, K);
+    } else {
+        if (feedback && quads)
+            launch_kind<KIND, BLOCK, HIT_LDS, GREC, true, true>(K, grid, lds, stream);
+        else if (feedback)
+            launch_kind<KIND, BLOCK, HIT_LDS, GREC, true, false>(K, grid, lds, stream);
+        else if (quads)
+            launch_kind<KIND, BLOCK, HIT_LDS, GREC, false, true>(K, grid, lds, stream);
+        else
+            launch_kind<KIND, BLOCK, HIT_LDS, GREC, false, false>(K, grid, lds, stream);
     }
+    std::snprintf(rt_launched_kernel, sizeof rt_launched_kernel, "%s<%d%s%s%s>%s",
+                  KIND == K_PAIR ? "rt_render_pair_kernel" : KIND == K_SORTED ? "rt_render_sorted_kernel" : "rt_render_kernel",
+                  KIND == K_PAIR ? 128 : BLOCK, HIT_LDS ? "" : ",hit_global", GREC ? ",grec" : "", BVH ? ",bvh" : "",
+                  feedback ? "+order" : "");
     hipError_t e = hipGetLastError();
     // the sort runs when asked, and always for a grid without an order yet
     if (e == hipSuccess && feedback && (K0.order_sort || K0.order_n != grid)) {
@@ -2272,7 +1667,7 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
 // The BVH instantiations live in their own translation unit
 // (rt_kernels_bvh.hip), built at -O3: the traversal loops want the full
 // optimizer while the brute-force kernels are faster at -O1.
-// BVH scenes by default: the ray-refill kernel, 64-lane groups (no barriers)
+// BVH scenes: the ray-refill kernel, 64-lane groups (no barriers)
 hipError_t rt_launch_render_bvh_refill(const rt_kparams& K0, int num_cus, hipStream_t s) {
     constexpr int BLOCK = 64;
     rt_kparams K = K0;
@@ -2304,6 +1699,8 @@ hipError_t rt_launch_render_bvh_refill(const rt_kparams& K0, int num_cus, hipStr
         hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, true>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
     else
         hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
+    std::snprintf(rt_launched_kernel, sizeof rt_launched_kernel, "rt_render_bvh_refill_kernel<64%s>%s",
+                  K.bvh_nodes16 ? ",n16" : "", feedback ? "+order" : "");
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && feedback && (K0.order_sort || K0.order_n != grid)) {
         e = rt_launch_order_groups(K0.group_cost, K0.group_order, grid, s);
@@ -2312,27 +1709,19 @@ hipError_t rt_launch_render_bvh_refill(const rt_kparams& K0, int num_cus, hipStr
     return e;
 }
 
-hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
-                                hipStream_t s) {
-    const bool grec = sorted && K.rec;
-    if (block == 64)
-        return grec ? launch_render<64, false, true, true, true>(K, lds, grid_mult, num_cus, s)
-                    : sorted ? launch_render<64, false, true, true>(K, lds, grid_mult, num_cus, s)
-                             : launch_render<64, false, false, true>(K, lds, grid_mult, num_cus, s);
-    if (block == 128)
-        return grec ? launch_render<128, false, true, true, true>(K, lds, grid_mult, num_cus, s)
-                    : sorted ? launch_render<128, false, true, true>(K, lds, grid_mult, num_cus, s)
-                             : launch_render<128, false, false, true>(K, lds, grid_mult, num_cus, s);
-    return grec ? launch_render<256, false, true, true, true>(K, lds, grid_mult, num_cus, s)
-                : sorted ? launch_render<256, false, true, true>(K, lds, grid_mult, num_cus, s)
-                         : launch_render<256, false, false, true>(K, lds, grid_mult, num_cus, s);
+// BVH scenes with samplesPerPixel > 1 (or BWRT_KERNEL=simple): the
+// one-path-per-lane kernel with the wave-synchronous BVH walk
+hipError_t rt_launch_render_bvh_simple(const rt_kparams& K, int block, size_t lds, int grid_mult, int num_cus,
+                                       hipStream_t s) {
+    return block == 64 ? launch_render<K_SIMPLE, 64, false, true>(K, lds, grid_mult, num_cus, s)
+                       : launch_render<K_SIMPLE, 256, false, true>(K, lds, grid_mult, num_cus, s);
 }
 #else
-hipError_t rt_launch_render_bvh(const rt_kparams& K, int block, bool sorted, size_t lds, int grid_mult, int num_cus,
-                                hipStream_t s);
+hipError_t rt_launch_render_bvh_simple(const rt_kparams& K, int block, size_t lds, int grid_mult, int num_cus,
+                                       hipStream_t s);
 hipError_t rt_launch_render_bvh_refill(const rt_kparams& K, int num_cus, hipStream_t s);
 
-size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted, int own = 0);
+size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted);
 // LDS bytes of one pair-kernel group (hit table in LDS)
 size_t rt_pair_lds_bytes(const rt_kparams& K) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
@@ -2341,36 +1730,24 @@ size_t rt_pair_lds_bytes(const rt_kparams& K) {
 }
 
 namespace {
-// spread: the sorted kernel with BLOCK / 2 pixels per group (LDS records,
-// hit table in LDS, brute force only; other launches ignore it)
-// spread 2: the pair kernel where it applies (128-lane groups)
-template <int BLOCK, bool SORTED>
-hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s,
-                        int spread = 0) {
-    if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
-        return rt_launch_render_bvh(K, BLOCK, SORTED, lds, grid_mult, num_cus, s);
-    if constexpr (SORTED && BLOCK == 128) {
-        if (spread == 2 && hit_lds && !K.rec)
-            return launch_render<128, true, true, false, false, 64, true>(K, rt_pair_lds_bytes(K), grid_mult, num_cus, s);
+template <int BLOCK, int KIND>
+hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_mult, int num_cus, hipStream_t s) {
+    if constexpr (KIND == K_SIMPLE) {
+        if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
+            return rt_launch_render_bvh_simple(K, BLOCK, lds, grid_mult, num_cus, s);
     }
-    if constexpr (SORTED && BLOCK >= 128) {
-        if (spread && hit_lds && !K.rec)
-            return launch_render<BLOCK, true, true, false, false, BLOCK / 2>(
-                K, rt_render_lds_bytes(K, BLOCK, true, true, BLOCK / 2), grid_mult, num_cus, s);
-    }
-    if (SORTED && K.rec)  // record stack in global memory
-        return hit_lds ? launch_render<BLOCK, true, SORTED, false, true>(K, lds, grid_mult, num_cus, s)
-                       : launch_render<BLOCK, false, SORTED, false, true>(K, lds, grid_mult, num_cus, s);
-    return hit_lds ? launch_render<BLOCK, true, SORTED, false>(K, lds, grid_mult, num_cus, s)
-                   : launch_render<BLOCK, false, SORTED, false>(K, lds, grid_mult, num_cus, s);
+    if (KIND == K_SORTED && K.rec)  // record stack in global memory
+        return hit_lds ? launch_render<KIND, BLOCK, true, false, true>(K, lds, grid_mult, num_cus, s)
+                       : launch_render<KIND, BLOCK, false, false, true>(K, lds, grid_mult, num_cus, s);
+    return hit_lds ? launch_render<KIND, BLOCK, true>(K, lds, grid_mult, num_cus, s)
+                   : launch_render<KIND, BLOCK, false>(K, lds, grid_mult, num_cus, s);
 }
 }  // namespace
 
 // Launch policy for the sorted kernel's record stack: global memory when the
 // LDS stack (3 dwords per level per lane) would hold the brute-force kernel
 // below RT_WAVES_PER_EU waves per SIMD, i.e. deep paths.  Measured: config
-// 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms; the BVH kernel
-// (VGPR-bound at 5 waves) 245 vs 255 ms, so it keeps LDS records.
+// 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms.
 // Also when global records let more 256-lane groups reside per CU (runtime
 // occupancy of both instantiations) and the frame runs at least
 // RT_GREC_MIN_GEN generations of them: config 3 (maxBounces 4) 6 -> 7
@@ -2393,8 +1770,8 @@ bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
     L.rec = reinterpret_cast<float*>(&L);  // any non-null: the global-record LDS size
     const size_t lds_g = rt_render_lds_bytes(L, 256, hit_lds, true);
     int occ_l = 0, occ_g = 0;
-    const void* kl = hit_lds ? kernel_ptr<256, true, true, false, false>() : kernel_ptr<256, false, true, false, false>();
-    const void* kg = hit_lds ? kernel_ptr<256, true, true, false, true>() : kernel_ptr<256, false, true, false, true>();
+    const void* kl = hit_lds ? kernel_ptr<K_SORTED, 256, true>() : kernel_ptr<K_SORTED, 256, false>();
+    const void* kg = hit_lds ? kernel_ptr<K_SORTED, 256, true, false, true>() : kernel_ptr<K_SORTED, 256, false, false, true>();
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_l, kl, 256, lds) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_g, kg, 256, lds_g) != hipSuccess || occ_g <= occ_l)
         return false;
@@ -2410,47 +1787,44 @@ bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
 size_t rt_render_rec_floats(const rt_kparams& K) {
     const long nitems = launch_items(K);
     const int lds_levels = K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS;
-    // (+ the deepest level with the deferred fold, RT_DEFER_FOLD)
-    const size_t planes = (size_t)3 * (K.max_bounces - lds_levels + (RT_DEFER_FOLD ? 1 : 0));
+    const size_t planes = (size_t)3 * (K.max_bounces - lds_levels);
     return planes ? planes * (size_t)((nitems + 255) / 256 * 256) : 1;
 }
 
 // LDS bytes of one workgroup: hit table (if staged) + 3 record dwords per
-// level per owner lane (own: pixels per group, 0 = block) + 13 task-slot
-// dwords per lane and 8 counters (sorted).
-size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted, int own) {
+// level per lane + 13 task-slot dwords per lane and 4 queue counters (sorted).
+size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool sorted) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
     const int lds_levels = sorted && K.rec ? (K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS)
                                            : K.max_bounces + (sorted ? 0 : 1);
-    size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * (own > 0 ? own : block) * sizeof(float);
-    if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);  // + counters, tail threshold
+    size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * block * sizeof(float);
+    if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);  // + queue counters
     return b;
 }
 
-// Host-side launch policy: 256-lane workgroups (64 when the record stack of
-// very deep paths would not fit), hit table in LDS when it fits in 16 KB,
-// sorted task-queue kernel unless `simple` (one pixel per lane: its grid
-// always covers every item); for the simple kernel grid_mult > 0 caps the
-// grid at grid_mult x resident workgroups per CU (persistent lanes).
-// spread_req: 1 / 0 forces the spread launch on / off (BWRT_SPREAD), -1 the
+// Host-side launch policy: BVH scenes take the ray-refill kernel; otherwise
+// 256-lane workgroups (64 when the record stack of very deep paths would not
+// fit), hit table in LDS when it fits in 16 KB, sorted task-queue kernel
+// unless `simple` (one pixel per lane: its grid always covers every item);
+// for the simple kernel grid_mult > 0 caps the grid at grid_mult x resident
+// workgroups per CU (persistent lanes).
+// pair_req: 1 / 0 forces the pair kernel on / off (BWRT_SPREAD), -1 the
 // policy: frames and shards of at most RT_SPREAD_PIX pixels per CU (about
-// 1.5 generations of the spread kernel's 7 waves per SIMD, 32 pixels per
-// wave) take 128-lane groups owning 64 pixels each.  Measured on c3 row
-// shards: 1/8 0.252 -> 0.227 ms, 1/16 0.254 -> 0.225 (256-lane groups owning
-// 128: 0.233, 0.234; profiles/r04/spread/ab_spread.txt); with the split
-// closest hit 1/6 (1,350 pixels per CU) 0.274 -> 0.248 but 1/4 (2,025) 0.270
-// -> 0.315 ms (profiles/r04/spread/ab_spread_mid.txt); 0 = off
+// 1.5 generations of 7 waves per SIMD, 32 pixels per wave) take 128-lane
+// pair groups owning 64 pixels each.  Measured on c3 row shards: 1/8 0.252
+// -> 0.194 ms, 1/16 0.254 -> 0.167 (profiles/r04g/shards_c3.txt); 1/4
+// (2,025 pixels per CU) keeps the sorted kernel
 #ifndef RT_SPREAD_PIX
 #define RT_SPREAD_PIX 1400
 #endif
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
-                            bool bvh_refill, hipStream_t stream, int spread_req, int pair_req) {
+                            hipStream_t stream, int pair_req) {
     // samplesPerPixel > 1 (the reference's in-frame loop, off by default):
     // only the one-path-per-lane kernel implements it
     simple = simple || K.spp_inner > 1;
-    if (K.bvh_nodes && bvh_refill && !simple && block_req == 0) return rt_launch_render_bvh_refill(K, num_cus, stream);
+    if (K.bvh_nodes && !simple) return rt_launch_render_bvh_refill(K, num_cus, stream);
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
 #ifdef RT_NO_HIT_LDS  // A/B builds: hit table read from global memory
     const bool hit_lds = false;
@@ -2461,27 +1835,25 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     const int block = small_block ? 64 : 256;
     const size_t lds = rt_render_lds_bytes(K, block, hit_lds, !simple);
     if (simple)
-        return small_block ? launch_block<64, false>(K, hit_lds, lds, grid_mult, num_cus, stream)
-                           : launch_block<256, false>(K, hit_lds, lds, grid_mult, num_cus, stream);
+        return small_block ? launch_block<64, K_SIMPLE>(K, hit_lds, lds, grid_mult, num_cus, stream)
+                           : launch_block<256, K_SIMPLE>(K, hit_lds, lds, grid_mult, num_cus, stream);
 #ifndef RT_SORTED_BLOCK
 #define RT_SORTED_BLOCK 256
 #endif
-    if (small_block) return launch_block<64, true>(K, hit_lds, lds, grid_mult, num_cus, stream);
+    if (small_block) return launch_block<64, K_SORTED>(K, hit_lds, lds, grid_mult, num_cus, stream);
+    const long items = (long)K.rows * K.width;
+    const bool pair = hit_lds && !K.rec && (block_req == 0 || block_req == 128) &&
+                      (pair_req > 0 || (pair_req < 0 && block_req == 0 && items <= (long)num_cus * RT_SPREAD_PIX));
+    if (pair)
+        return launch_render<K_PAIR, 128, true>(K, rt_pair_lds_bytes(K), grid_mult, num_cus, stream);
     if (block_req == 64 || block_req == 128 || block_req == 256) {  // explicit (BWRT_BLOCK)
         const size_t lds_r = rt_render_lds_bytes(K, block_req, hit_lds, true);
         if (lds_r <= 65536) {
-            const int spread = spread_req > 0 ? (pair_req && block_req == 128 ? 2 : 1) : 0;
-            if (block_req == 64) return launch_block<64, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
-            if (block_req == 128)
-                return launch_block<128, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream, spread);
-            return launch_block<256, true>(K, hit_lds, lds_r, grid_mult, num_cus, stream, spread);
+            if (block_req == 64) return launch_block<64, K_SORTED>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
+            if (block_req == 128) return launch_block<128, K_SORTED>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
+            return launch_block<256, K_SORTED>(K, hit_lds, lds_r, grid_mult, num_cus, stream);
         }
     }
-    // BVH traversal: node-loop lengths differ widely between waves and a
-    // group waits for its slowest wave at every round's barriers, so the BVH
-    // kernels run single-wave groups (config 5: 246 -> 215 ms; 128 lanes: 226)
-    if (K.bvh_nodes) return launch_block<64, true>(K, hit_lds, rt_render_lds_bytes(K, 64, hit_lds, true), grid_mult,
-                                                   num_cus, stream);
     const size_t lds_s = rt_render_lds_bytes(K, RT_SORTED_BLOCK, hit_lds, true);
     // deep paths (large max_bounces) make the LDS record stack big: take
     // 128-lane groups when they keep more waves resident per CU (LDS 160 KB,
@@ -2494,23 +1866,19 @@ hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, boo
     // full-size groups per CU leave CUs with unequal shares of the critical
     // path (every group is resident at once); 128-lane groups spread it
     // (measured on c3 row shards of 1/8: 0.249 vs 0.264 ms; 1/4: 0.312 vs
-    // 0.291), and spread launches (above) spread it further
-    const long items = (long)K.rows * K.width;
+    // 0.291), and the pair kernel (above) spreads it further
     const bool few_groups = items < (long)num_cus * 4 * RT_SORTED_BLOCK;
-    const bool spread = spread_req > 0 || (spread_req < 0 && items <= (long)num_cus * RT_SPREAD_PIX);
-    if (spread)  // (launch_block sizes a spread launch's LDS itself; this size is for those it cannot spread)
-        return launch_block<128, true>(K, hit_lds, rt_render_lds_bytes(K, 128, hit_lds, true), grid_mult, num_cus, stream,
-                                       pair_req ? 2 : 1);
     if (RT_SORTED_BLOCK > 128 &&
         (few_groups ||
          waves_per_cu(rt_render_lds_bytes(K, 128, hit_lds, true), 128) > waves_per_cu(lds_s, RT_SORTED_BLOCK))) {
         const size_t lds_128 = rt_render_lds_bytes(K, 128, hit_lds, true);
-        return launch_block<128, true>(K, hit_lds, lds_128, grid_mult, num_cus, stream);
+        return launch_block<128, K_SORTED>(K, hit_lds, lds_128, grid_mult, num_cus, stream);
     }
-    return launch_block<RT_SORTED_BLOCK, true>(K, hit_lds, lds_s, grid_mult, num_cus, stream);
+    return launch_block<RT_SORTED_BLOCK, K_SORTED>(K, hit_lds, lds_s, grid_mult, num_cus, stream);
 }
 
 thread_local long rt_order_groups_last = 0;
+thread_local char rt_launched_kernel[96] = "";
 
 hipError_t rt_launch_order_groups(const unsigned* cost, int* order, long n, hipStream_t stream) {
     hipLaunchKernelGGL(rt_order_groups_kernel, dim3(1), dim3(1024), 0, stream, cost, order, (int)n);

@@ -125,20 +125,7 @@ struct rt_kparams {
     // frame's sample.  1 (the reference build) everywhere but the simple
     // kernel and the CPU fallback, which the launch policy picks for n > 1
     int spp_inner;
-    // sorted kernel, brute-force scenes: once a workgroup holds at most
-    // tail_n live pixels (<= RT_TAIL_MAX) each wave finishes its own without
-    // barriers, several lanes per pixel splitting each closest hit
-    // (rt_kernels.hip, "tail"); 0 = off
-    int tail_n;
 };
-
-// tail mode: at most this many pixels per workgroup, and the LDS words of a
-// wave's hand-off record (fields x pixels, in the task-slot area)
-#define RT_TAIL_MAX 16
-#define RT_TAIL_FIELDS 28
-#ifndef RT_TAIL_N
-#define RT_TAIL_N 0  // launch policy: off (measured: no gain on the c3 shards, tools/ab_tail.sh)
-#endif
 
 // leaf-batch thresholds of the launch policy (full frames / small shards)
 #ifndef RT_LEAF_BATCH

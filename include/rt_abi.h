@@ -39,8 +39,7 @@
  *    result, only kernel choice and speed:
  *      at rt_create:    BWRT_KERNEL=simple, BWRT_BLOCK, BWRT_TILE, BWRT_TILE_SQ,
  *                       BWRT_GREC, BWRT_GRID_MULT, BWRT_LEAF_BATCH, BWRT_REFILL,
- *                       BWRT_TAIL, BWRT_SPREAD, BWRT_PAIR, BWRT_BVH_REFILL, BWRT_ORDER,
- *                       BWRT_ORDER_PERIOD
+ *                       BWRT_SPREAD, BWRT_ORDER, BWRT_ORDER_PERIOD
  *      at rt_set_scene: BWRT_BVH_MIN, BWRT_BVH_LEAF, BWRT_BVH_CT, BWRT_BVH_SBVH,
  *                       BWRT_BVH_REFS, BWRT_BVH_ALPHA, BWRT_BVH_ORDER_MASK,
  *                       BWRT_BVH_N16, BWRT_NO_CULL, BWRT_BVH_STATS (report)
@@ -308,8 +307,11 @@ RT_API int rt_render_device(rt_context* ctx, const rt_render_params* p,
  * NULL) record their completion event lazily — when a later call needs it:
  * a render on another stream, a state read or write, rt_synchronize — so
  * back-to-back renders carry no marker packet between them (1.5-3 us per
- * launch on MI355X).  A render on a caller's stream records it at once (the
- * caller may destroy that stream). */
+ * launch on MI355X).  Such a deferred event is recorded at the end of the
+ * stream when the later call comes, so it also covers any work the caller
+ * queued on this stream after the render (a gather, a copy): calls that wait
+ * for the render wait for that work too.  A render on a caller's stream
+ * records it at once (the caller may destroy that stream). */
 RT_API void* rt_get_stream(rt_context* ctx);
 
 /* Wait for all work of the context: its stream, the last render launch
@@ -335,6 +337,15 @@ RT_API int rt_render_multi(rt_context* const* ctxs, int n, int width, int height
  * launch; -1 when unavailable (no render yet, or kernel timing off).
  * Synchronises on that launch's end event. */
 RT_API float rt_last_kernel_ms(rt_context* ctx);
+
+/* Name of the render kernel the context's last GPU render launched, with
+ * its workgroup lanes and variant, e.g. "rt_render_sorted_kernel<256,grec>+order"
+ * (full frames), "rt_render_pair_kernel<128>+order" (small frames and
+ * shards), "rt_render_bvh_refill_kernel<64,n16>" (BVH scenes); "" before
+ * the first render and on a CPU context.  A diagnostic of the launch
+ * policy (tests assert which kernel a workload runs); valid until the next
+ * render on the context.  The reference launches one kernel, Main.cu:342. */
+RT_API const char* rt_last_kernel_name(const rt_context* ctx);
 
 /* Per-launch kernel timing (default on): every render records a start event
  * before its kernels; its end event (recorded either way: later calls are

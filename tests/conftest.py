@@ -18,14 +18,28 @@ for p in (REPO, os.path.join(REPO, "bwidman-raytracer_amd"), os.path.join(REPO, 
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
-# the tests force launch knobs (BWRT_BLOCK, BWRT_GREC, BWRT_TAIL, ...): the
+# the tests force launch knobs (BWRT_BLOCK, BWRT_GREC, BWRT_SPREAD, ...): the
 # library reads them only under BWRT_TUNING=1 (test_host_io checks the gate)
 os.environ.setdefault("BWRT_TUNING", "1")
+# a stray knob in the caller's environment would change which kernel every
+# default-policy test checks: only the tests themselves set them (BWRT_LIB
+# picks the library, BWRT_TUNING opens the gate)
+for _k in [k for k in os.environ if k.startswith("BWRT_") and k not in ("BWRT_LIB", "BWRT_TUNING")]:
+    del os.environ[_k]
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libbwrt.so / HIP)")
     config.addinivalue_line("markers", "slow: long CPU oracle runs")
+
+
+@pytest.fixture(autouse=True)
+def _no_stray_knobs():
+    """Knobs a test sets through monkeypatch are undone by it; this catches
+    any left behind by a test that set os.environ directly."""
+    yield
+    for k in [k for k in os.environ if k.startswith("BWRT_") and k not in ("BWRT_LIB", "BWRT_TUNING")]:
+        del os.environ[k]
 
 
 @pytest.fixture(scope="session")

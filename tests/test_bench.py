@@ -1,0 +1,69 @@
+"""bench.py's launch logic (CPU): a plain `python bench.py --gpus N` must
+start its own N ranks (torch.distributed.run on 127.0.0.1) before anything
+touches the GPU, forward their exit status, and never re-exec itself; a rank
+started by torch.distributed.run (WORLD_SIZE set) runs the benchmark."""
+import importlib.util
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_self_launch_command(bench):
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+    cmd, env = bench.self_launch_command(argv, 8, 29123)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=8" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29123" in cmd
+    script = cmd.index(os.path.join(REPO, "bench.py"))
+    assert cmd[script + 1:] == argv  # the same arguments reach every rank
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert "WORLD_SIZE" not in env or env["WORLD_SIZE"] == os.environ.get("WORLD_SIZE")
+
+
+@pytest.mark.parametrize("rc", [0, 3])
+def test_plain_launch_spawns_ranks_and_forwards_status(bench, monkeypatch, rc):
+    calls = []
+
+    class Done:
+        returncode = rc
+
+    def fake_run(cmd, env=None, **kw):
+        calls.append((cmd, env))
+        return Done()
+
+    def no_gpu(*a, **k):
+        raise AssertionError("the launcher process must not touch the GPU")
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(bench.torch.cuda, "set_device", no_gpu)
+    monkeypatch.setattr(bench.os, "execv", no_gpu)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == rc
+    assert len(calls) == 1
+    cmd, env = calls[0]
+    assert "--nproc-per-node=2" in cmd and cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+
+
+def test_rank_under_torchrun_does_not_relaunch(bench, monkeypatch):
+    """WORLD_SIZE set (a torch.distributed.run rank): no child launch; a
+    mismatch with --gpus is an error, not a relaunch."""
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setattr(bench.subprocess, "run", lambda *a, **k: pytest.fail("relaunched"))
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert "WORLD_SIZE=4" in str(e.value.code)

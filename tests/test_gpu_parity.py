@@ -54,8 +54,29 @@ def test_07_small(gpu, oracle, w, h, spp, mb):
 
 
 def test_config3_07_full_size(gpu, oracle):
-    """BASELINE config 3 exactly: 07 scene, 1920x1080, 8 spp, 4 bounces."""
+    """BASELINE config 3 exactly: 07 scene, 1920x1080, 8 spp, 4 bounces, through
+    the launch policy's kernel for it (the bench's kernel)."""
     img, st = run_pair(gpu, oracle, scenes.scene_07(), 1920, 1080, 8, 4)
+    assert gpu.last_kernel_name().startswith("rt_render_sorted_kernel<256,grec>"), gpu.last_kernel_name()
+    assert np.array_equal(img, st.rgba)
+    same_state(gpu, st)
+
+
+# the per-rank workloads of the headline metric's 2 / 4 / 8-GPU points
+# (rank r of G renders rows y = r mod G), plus 6 rows apart, the pair kernel's
+# boundary (345,600 pixels <= 256 CUs x RT_SPREAD_PIX 1,400), each through the
+# DEFAULT launch policy and the kernel it picks for that shard
+@pytest.mark.parametrize("stride,offset,kernel", [(2, 1, "rt_render_sorted_kernel<256>"),
+                                                  (4, 3, "rt_render_sorted_kernel<256>"),
+                                                  (6, 2, "rt_render_pair_kernel<128>"),
+                                                  (8, 5, "rt_render_pair_kernel<128>")])
+def test_config3_shards(gpu, oracle, stride, offset, kernel):
+    """Config 3 (07, 1920x1080, 8 spp, 4 bounces) as one rank's row shard of
+    a G-GPU frame: RGBA, frameSum and RNG bit-exact with the oracle on the
+    same rows (the global-index seeds make shards exact, Main.cu:377)."""
+    img, st = run_pair(gpu, oracle, scenes.scene_07(), 1920, 1080, 8, 4, row_offset=offset, row_stride=stride)
+    assert gpu.last_kernel_name().startswith(kernel), gpu.last_kernel_name()
+    assert img.shape[0] == len(range(offset, 1080, stride))
     assert np.array_equal(img, st.rgba)
     same_state(gpu, st)
 
@@ -767,61 +788,43 @@ def test_global_records_forced(bwrt_lib, oracle, monkeypatch, block, w, h, mb):
         r.close()
 
 
-@pytest.mark.parametrize("block", [64, 128, 256])
-@pytest.mark.parametrize("tail", [0, 1, 5, 16])
-@pytest.mark.parametrize("grec", [0, 1])
-def test_tail_mode_forced(bwrt_lib, oracle, monkeypatch, block, tail, grec):
-    """The sorted kernel's tail mode (a group's last <= BWRT_TAIL live pixels
-    finished by its first wave, several lanes per pixel splitting each closest
-    hit) at every workgroup size and with LDS / global records: the 07 scene
-    (shared pyramid edges: exact ties between triangles), the quad box, a
-    seeded random scene, and one scaled by 1e10 (rays whose tests could
-    overflow take the serial loop inside the tail).  tail 0 = off."""
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_TAIL=tail, BWRT_BLOCK=block, BWRT_GREC=grec)
-    cases = [(scenes.scene_07(), 160, 90, 3, 4, 0, 1), (scenes.scene_04_box(), 96, 61, 2, 5, 1, 3),
-             (_random_scene(7), 80, 45, 2, 6, 0, 1), (_scaled(_random_scene(3), 1e10), 64, 36, 2, 5, 0, 1)]
+@pytest.mark.parametrize("spread", [1, 0])
+def test_pair_kernel_forced_on_off(bwrt_lib, oracle, monkeypatch, spread):
+    """BWRT_SPREAD=1 forces the pair kernel (128-lane groups for 64 pixels:
+    an owner wave and a helper wave that runs the SPEC tasks and half of
+    every closest hit); BWRT_SPREAD=0 keeps small frames, which the policy
+    gives to the pair kernel, on the sorted kernel (128-lane groups).
+    Ragged sizes (the last group part-owned), a one-pixel frame, row shards,
+    quads, exact ties, and a scene scaled by 1e10 (rays that fail bvh_safe:
+    the whole loop on the owner)."""
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=spread)
+    cases = [(scenes.scene_07(), 160, 90, 3, 4, 0, 1), (scenes.scene_04_box(), 96, 61, 2, 4, 1, 3),
+             (_random_scene(7), 81, 45, 2, 3, 0, 1), (scenes.scene_07(), 1, 1, 2, 4, 0, 1),
+             (_scaled(_random_scene(3), 1e10), 64, 36, 2, 4, 0, 1), (scenes.scene_04_box(), 96, 61, 2, 6, 0, 1)]
     try:
         for scene, w, h, spp, mb, off, stride in cases:
             img, st = run_pair(r, oracle, scene, w, h, spp, mb, row_offset=off, row_stride=stride)
             assert np.array_equal(img, st.rgba)
             same_state(r, st)
+            # (max_bounces >= 5: the policy keeps the deep record stack in
+            # global memory, which only the sorted kernel has)
+            want = "rt_render_pair_kernel<128>" if spread and mb <= 4 else "rt_render_sorted_kernel<128"
+            assert r.last_kernel_name().startswith(want), r.last_kernel_name()
     finally:
         r.close()
 
 
-@pytest.mark.parametrize("block,pair", [(128, 1), (128, 0), (256, 1)])
-def test_spread_launch_forced(bwrt_lib, oracle, monkeypatch, block, pair):
-    """Spread launches (BWRT_SPREAD=1): block / 2 pixels per workgroup.  128
-    lanes: the pair kernel (owner wave + helper wave: diffuse bounces in
-    place, SPEC tasks and half of every closest hit on the helper), or with
-    BWRT_PAIR=0 the sorted kernel with a split closest hit; 256 lanes: the
-    sorted kernel, two owner waves.  Ragged sizes (the last group
-    part-owned), a one-pixel frame, row shards, quads, exact ties, and a
-    scene scaled by 1e10 (rays that fail bvh_safe: the whole loop)."""
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block, BWRT_PAIR=pair)
-    cases = [(scenes.scene_07(), 160, 90, 3, 4, 0, 1), (scenes.scene_04_box(), 96, 61, 2, 5, 1, 3),
-             (_random_scene(7), 81, 45, 2, 6, 0, 1), (scenes.scene_07(), 1, 1, 2, 4, 0, 1),
-             (_scaled(_random_scene(3), 1e10), 64, 36, 2, 5, 0, 1)]
-    try:
-        for scene, w, h, spp, mb, off, stride in cases:
-            img, st = run_pair(r, oracle, scene, w, h, spp, mb, row_offset=off, row_stride=stride)
-            assert np.array_equal(img, st.rgba)
-            same_state(r, st)
-    finally:
-        r.close()
-
-
-@pytest.mark.parametrize("block,pair", [(128, 1), (128, 0), (256, 1)])
-def test_spread_launch_order_feedback(bwrt_lib, oracle, monkeypatch, block, pair):
-    """A spread launch on a multi-generation grid (07 at 1080p, block / 2
+def test_pair_kernel_order_feedback(bwrt_lib, oracle, monkeypatch):
+    """The pair kernel forced on a multi-generation grid (07 at 1080p, 64
     pixels per group) with launch-order feedback: blockIdx order, then
     reordered twice; every frame equals the oracle."""
     w, h, mb = 1920, 1080, 4
     scene = scenes.scene_07()
     st = oracle.OracleState(w, h)
     oracle.render(scene, st, 1, mb, first_frame=1)
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_BLOCK=block, BWRT_PAIR=pair, BWRT_ORDER=1,
-                        BWRT_ORDER_PERIOD=2)
+    # (BWRT_GREC=0: a full frame would take global records, which the pair
+    # kernel does not have)
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_SPREAD=1, BWRT_ORDER=1, BWRT_ORDER_PERIOD=2, BWRT_GREC=0)
     try:
         r.set_scene(scene)
         for _ in range(3):
@@ -829,6 +832,7 @@ def test_spread_launch_order_feedback(bwrt_lib, oracle, monkeypatch, block, pair
             img = r.render(w, h, 1, mb, first_frame=1)
             assert np.array_equal(img, st.rgba)
             same_state(r, st)
+        assert r.last_kernel_name() == "rt_render_pair_kernel<128>+order", r.last_kernel_name()
     finally:
         r.close()
 
@@ -843,23 +847,6 @@ def test_simple_kernel_ab_reference(bwrt_lib, oracle, monkeypatch, name):
         assert np.array_equal(img, st.rgba)
         same_state(r, st)
     finally:
-        r.close()
-
-
-@pytest.mark.parametrize("name", ["stress", "07"])
-def test_bvh_through_sorted_kernel(bwrt_lib, oracle, monkeypatch, name):
-    """BVH scenes through the sorted task-queue kernel (BWRT_BVH_REFILL=0)
-    instead of the default ray-refill kernel; the 07 scene with the BVH
-    forced (shared pyramid edges: exact ties)."""
-    monkeypatch.setenv("BWRT_BVH_MIN", "1")
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_BVH_REFILL=0)
-    scene, w, h, mb = ((scenes.stress_scene(), 96, 54, 8) if name == "stress" else (scenes.scene_07(), 200, 113, 5))
-    try:
-        img, st = run_pair(r, oracle, scene, w, h, 2, mb)
-        assert np.array_equal(img, st.rgba)
-        same_state(r, st)
-    finally:
-        monkeypatch.delenv("BWRT_BVH_MIN")
         r.close()
 
 

@@ -1,6 +1,7 @@
 """Extreme-scale parity probe: the stress scene scaled by 1e10 / 1e6 through the BVH and the
 brute-force loop against the oracle (pixels, RNG and accumulators that differ).  GPU box only."""
 import os, sys
+os.environ["BWRT_TUNING"] = "1"  # the library reads BWRT_* knobs only under it
 sys.path[:0] = ["bwidman-raytracer_amd", "oracle", "tests"]
 import numpy as np
 import oracle as O

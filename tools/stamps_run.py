@@ -1,4 +1,5 @@
 import os, sys
+os.environ["BWRT_TUNING"] = "1"  # the library reads BWRT_* knobs only under it
 sys.path[:0] = ["bwidman-raytracer_amd"]
 import torch
 from bwrt import Renderer, abi, scenes

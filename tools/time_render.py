@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Median kernel time of one render on GPU 0: tools/time_render.py SCENE W H SPP MB [REPS]
-(launch knobs from the BWRT_* environment, read when the context is made)."""
+(launch knobs from the BWRT_* environment, read when the context is made and
+only under BWRT_TUNING=1, which this script sets)."""
 import os
+os.environ["BWRT_TUNING"] = "1"
 import statistics
 import sys
 
