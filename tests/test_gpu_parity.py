@@ -66,8 +66,8 @@ def test_config3_07_full_size(gpu, oracle):
 # (rank r of G renders rows y = r mod G), plus 6 rows apart, the pair kernel's
 # boundary (345,600 pixels <= 256 CUs x RT_SPREAD_PIX 1,400), each through the
 # DEFAULT launch policy and the kernel it picks for that shard
-@pytest.mark.parametrize("stride,offset,kernel", [(2, 1, "rt_render_sorted_kernel<256>"),
-                                                  (4, 3, "rt_render_sorted_kernel<256>"),
+@pytest.mark.parametrize("stride,offset,kernel", [(2, 1, "rt_render_sorted_kernel<256"),
+                                                  (4, 3, "rt_render_sorted_kernel<256"),
                                                   (6, 2, "rt_render_pair_kernel<128>"),
                                                   (8, 5, "rt_render_pair_kernel<128>")])
 def test_config3_shards(gpu, oracle, stride, offset, kernel):
