@@ -278,12 +278,6 @@ __device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
 #ifndef RT_PAIR_WAVES
 #define RT_PAIR_WAVES 7
 #endif
-// pair kernel: a round's SPEC tasks run on two helper lanes each (the two
-// sincos of the microfacet sample and the two G1 terms on partner lanes)
-// when at most 32 are posted
-#ifndef RT_PAIR_SPEC2
-#define RT_PAIR_SPEC2 0
-#endif
 
 template <int BLOCK, bool HIT_LDS, bool BVH>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
@@ -544,56 +538,6 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __
 
 
 enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };  // a lane's next task
-
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) {
-    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false);
-}
-
-// specular_scatter (rt_path.h, Main.cu:245-255) on two partner lanes that
-// hold the same task (sl = 0 / 1, lanes 2k and 2k+1): the two sincos_nn of
-// the microfacet sample and the two G1 terms of specularWeight each run on
-// one lane and are exchanged with a DPP quad_perm [1,0,3,2], so the task's
-// dependency chain carries one of each.  Same operations on the same
-// operands, same results (a float product is commutative).
-__device__ __forceinline__ f3 specular_scatter_pair(Xorwow& rs, f3 d, f3 n, float rough, float rough2, float ior2m1,
-                                                    float& kspec, int sl) {
-    const bool odd = sl & 1;
-    const float e1 = rand_range(rs, 1.0f);
-    const float e2 = rand_range(rs, 1.0f);
-    const float theta = atan_nn(rough * rt_sqrt(e1) / rt_sqrt(1.0f - e1));
-    const float phi = 2.0f * RT_PI * e2;
-    float s_, c_;
-    sincos_nn(odd ? phi : theta, s_, c_);
-    const float s2 = __int_as_float(dpp_i<0xB1>(__float_as_int(s_)));
-    const float c2 = __int_as_float(dpp_i<0xB1>(__float_as_int(c_)));
-    const float st = odd ? s2 : s_, ct = odd ? c2 : c_;  // theta's, from the even lane
-    const float sp = odd ? s_ : s2, cp = odd ? c_ : c2;  // phi's, from the odd lane
-    const f3 mloc = mk(st * cp, st * sp, ct);
-    f3 some = mk(1.0f, 0.0f, 0.0f);
-    if (fabsf(dot(n, some)) < 1.0f - RT_NEAR_ZERO) some = mk(0.0f, 1.0f, 0.0f);
-    const f3 t1 = cross(n, some);
-    const f3 t2 = cross(n, t1);
-    const f3 m = mk(dot(mk(t1.x, t2.x, n.x), mloc), dot(mk(t1.y, t2.y, n.y), mloc), dot(mk(t1.z, t2.z, n.z), mloc));
-    const f3 scatter = sub(d, scale(2.0f * dot(d, m), m));
-    const f3 inc = scale(-1.0f, d);
-    const float fr = fresnel(inc, m, ior2m1);
-    // specular_weight(inc, scatter, n, m, rough2): G1(inc) on the even lane,
-    // G1(scatter) on the odd one
-    const float g1 = shadowing_masking(odd ? scatter : inc, n, m, rough2);
-    const float g1p = __int_as_float(dpp_i<0xB1>(__float_as_int(g1)));
-    const float g = g1 * g1p;
-    float sw;
-    if (isnan(g)) {
-        sw = 1.0f;
-    } else {
-        float den = fabsf(dot(inc, n) * dot(m, n));
-        if (den == 0.0f) den = RT_NEAR_ZERO;
-        sw = fabsf(dot(inc, m)) * g / den;
-    }
-    kspec = sw * fr / RT_SPECULAR_CHANCE;
-    return scatter;
-}
 
 // ===========================================================================
 // Sorted task-queue megakernel (the product path).
@@ -1070,11 +1014,9 @@ rt_render_pair_kernel(rt_kparams K) {
     // scattered direction out, 15 SPEC kspec out, 16-21 RNG state (SPEC in /
     // out), 22 SPEC flag (1 posted, 3 posted and its ray traced), 23-24 the
     // owner's (t, id)
-    lds_float* const xbase = (lds_float*)(rec_base + 3 * levels * 64);
-    lds_float* xb = xbase + j;
+    lds_float* xb = (lds_float*)(rec_base + 3 * levels * 64) + j;
 #define XF(f) xb[(f) * 64]
     int* live_flag = reinterpret_cast<int*>(rec_base + 3 * levels * 64 + RT_PAIR_FIELDS * 64);
-    int* spec_list = live_flag + 4;  // (RT_PAIR_SPEC2) pixels of the round's SPEC tasks
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
 #ifdef RT_GTIMES
@@ -1161,70 +1103,38 @@ rt_render_pair_kernel(rt_kparams K) {
                 XF(6) = __int_as_float(flag);
             }
         } else {
-#if RT_PAIR_SPEC2
-            // the round's SPEC tasks on lane pairs: the k-th runs on lanes
-            // 2k and 2k + 1, 32 at a time (their pixels listed in LDS by this
-            // wave and read back by it)
-            const int sf0 = __float_as_int(XF(22));
-            const unsigned long long ms = __ballot(sf0 & 1);
-            const int ns = __popcll(ms);
-            if (sf0 & 1) spec_list[lanes_below(ms)] = j;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            const int sl = j & 1;
-            for (int kb = 0; kb < ns; kb += 32) {  // (wave-uniform)
-                const int k = kb + (j >> 1);
-                const int q = k < ns ? spec_list[k] : j;
-                const int hq = __shfl(hid, q);  // (every helper lane active here)
-                lds_float* const xq = xbase + q;
-#define XQ(f) xq[(f) * 64]
-                const int sf = k < ns ? __float_as_int(XQ(22)) : 0;
-#else
-            {
-                const int sf = __float_as_int(XF(22));
-                const int hq = hid;
-#define XQ(f) XF(f)
-#endif
-                if (sf & 1) {  // the owner's SPEC task, Main.cu:245-255
-                    Xorwow rs;
-                    rs.d = __float_as_uint(XQ(16));
-                    rs.v0 = __float_as_uint(XQ(17));
-                    rs.v1 = __float_as_uint(XQ(18));
-                    rs.v2 = __float_as_uint(XQ(19));
-                    rs.v3 = __float_as_uint(XQ(20));
-                    rs.v4 = __float_as_uint(XQ(21));
-                    const f3 nrm = mk(XQ(9), XQ(10), XQ(11));
-                    const f3 dd = mk(XQ(3), XQ(4), XQ(5));  // the incoming ray
-                    const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * hq + 8);
-                    float kspec;
-#if RT_PAIR_SPEC2
-                    const f3 r = specular_scatter_pair(rs, dd, nrm, h2.x, h2.z, h2.y, kspec, sl);
-                    if (sl == 0) {
-#else
-                    const f3 r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
-                    {
-#endif
-                        XQ(12) = r.x;
-                        XQ(13) = r.y;
-                        XQ(14) = r.z;
-                        XQ(15) = kspec;
-                        XQ(16) = __uint_as_float(rs.d);
-                        XQ(17) = __uint_as_float(rs.v0);
-                        XQ(18) = __uint_as_float(rs.v1);
-                        XQ(19) = __uint_as_float(rs.v2);
-                        XQ(20) = __uint_as_float(rs.v3);
-                        XQ(21) = __uint_as_float(rs.v4);
-                        int flag = 0;
-                        if (sf & 2) {  // traced: the ray from the hit point (posted in XF(0..2))
-                            XQ(3) = r.x;
-                            XQ(4) = r.y;
-                            XQ(5) = r.z;
-                            flag = bvh_safe(K, mk(XQ(0), XQ(1), XQ(2)), r) ? 1 : 2;
-                        }
-                        XQ(6) = __int_as_float(flag);
-                    }
+            const int sf = __float_as_int(XF(22));
+            if (sf & 1) {  // the owner's SPEC task, Main.cu:245-255
+                Xorwow rs;
+                rs.d = __float_as_uint(XF(16));
+                rs.v0 = __float_as_uint(XF(17));
+                rs.v1 = __float_as_uint(XF(18));
+                rs.v2 = __float_as_uint(XF(19));
+                rs.v3 = __float_as_uint(XF(20));
+                rs.v4 = __float_as_uint(XF(21));
+                const f3 nrm = mk(XF(9), XF(10), XF(11));
+                const f3 dd = mk(XF(3), XF(4), XF(5));  // the incoming ray
+                const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * hid + 8);
+                float kspec;
+                const f3 r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
+                XF(12) = r.x;
+                XF(13) = r.y;
+                XF(14) = r.z;
+                XF(15) = kspec;
+                XF(16) = __uint_as_float(rs.d);
+                XF(17) = __uint_as_float(rs.v0);
+                XF(18) = __uint_as_float(rs.v1);
+                XF(19) = __uint_as_float(rs.v2);
+                XF(20) = __uint_as_float(rs.v3);
+                XF(21) = __uint_as_float(rs.v4);
+                int flag = 0;
+                if (sf & 2) {  // traced: the ray from the hit point (posted in XF(0..2))
+                    XF(3) = r.x;
+                    XF(4) = r.y;
+                    XF(5) = r.z;
+                    flag = bvh_safe(K, mk(XF(0), XF(1), XF(2)), r) ? 1 : 2;
                 }
-#undef XQ
+                XF(6) = __int_as_float(flag);
             }
         }
         __syncthreads();
@@ -1816,8 +1726,7 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
 size_t rt_pair_lds_bytes(const rt_kparams& K) {
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     return (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) +
-           (size_t)(3 * (K.max_bounces > 0 ? K.max_bounces : 0) + RT_PAIR_FIELDS) * 64 * sizeof(float) +
-           (RT_PAIR_SPEC2 ? 68 : 4) * sizeof(int);
+           (size_t)(3 * (K.max_bounces > 0 ? K.max_bounces : 0) + RT_PAIR_FIELDS) * 64 * sizeof(float) + 4 * sizeof(int);
 }
 
 namespace {
