@@ -4,7 +4,7 @@ import collections, csv, glob, json, os, sys
 def load(outdir, kernel_sub="rt_render"):
     vals = collections.defaultdict(list)
     durs = []
-    for f in sorted(glob.glob(os.path.join(outdir, "pass*", "run_counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(outdir, "pass*", "run_counter_collection.csv")) + glob.glob(os.path.join(outdir, "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             if kernel_sub in r["Kernel_Name"]:
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
