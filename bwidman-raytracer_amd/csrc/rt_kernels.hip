@@ -311,35 +311,7 @@ rt_render_kernel(rt_kparams K) {
     f3 dcam = d;
     int inner = 1;
 
-#ifdef RT_STAMPS
-    unsigned long long st_acc[5] = {0, 0, 0, 0, 0};
-#define STAMP(k)                                              \
-    do {                                                      \
-        unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-        st_acc[k] += _t - st_prev;                            \
-        st_prev = _t;                                         \
-    } while (0)
-    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
-    // utilisation counters (wave-level, lane 0 adds): [0] rounds, [1] front
-    // waves, [2] front tasks, [3] rejection-loop wave trips, [4] rejection
-    // lane trips, [5] spec waves, [6] spec tasks, [7] I-phase waves,
-    // [8] I-phase rays
-    unsigned long long st_u[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    auto wave_max = [](int v) {
-        for (int m = 1; m < 64; m <<= 1) v = max(v, __shfl_xor(v, m));
-        return v;
-    };
-    auto wave_sum = [](int v) {
-        for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
-        return v;
-    };
-#else
-#define STAMP(k) \
-    do {         \
-    } while (0)
-#endif
     while (true) {
-        STAMP(4);
         // (1) regenerate: jittered camera ray (Main.cu:290-292)
         if (depth < 0 && px.passes_left > 0) {
             f3 jit = random_direction(px.rs, px.d0);
@@ -349,7 +321,6 @@ rt_render_kernel(rt_kparams K) {
             dcam = d;
             inner = K.spp_inner;
         }
-        STAMP(0);
         const bool active = depth >= 0;
         if (__ballot(active) == 0ull) break;
         if (active) {
@@ -357,7 +328,6 @@ rt_render_kernel(rt_kparams K) {
             float t;
             int id;
             closest_hit<BVH>(K, o, d, t, id);
-            STAMP(1);
 
             bool finished = true;
             if (id >= 0) {
@@ -411,7 +381,6 @@ rt_render_kernel(rt_kparams K) {
                 d = scatter;
                 finished = depth > K.max_bounces;  // Main.cu:210
             }
-            STAMP(2);
             if (finished) {
                 // (4) fold the recursion innermost-first (Main.cu:262-268):
                 //     L = emitted + (brdf * L) * cosAngle
@@ -448,14 +417,8 @@ rt_render_kernel(rt_kparams K) {
                     load_item(K, npix, nitems, px.w + T, px);
                 }
             }
-            STAMP(3);
         }
     }
-#ifdef RT_STAMPS
-    if ((threadIdx.x & 63) == 0 && K.stamps)
-        for (int k = 0; k < 5; k++) atomicAdd(&K.stamps[k], st_acc[k]);
-#endif
-#undef STAMP
 }
 
 #ifndef RT_TU_BVH  // defined once, in the main translation unit
