@@ -1714,11 +1714,12 @@ hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_
 // Also when global records let more 256-lane groups reside per CU (runtime
 // occupancy of both instantiations) and the frame runs at least
 // RT_GREC_MIN_GEN generations of them: config 3 (maxBounces 4) 6 -> 7
-// waves/SIMD, 0.816 -> 0.801 ms (three alternating runs); its row shards of
-// 1/2 .. 1/16 (1.1 - 2.3 generations) lose 2 - 7 % with global records and
-// config 2 gains no group, so both keep LDS records
+// waves/SIMD, 0.816 -> 0.801 ms (three alternating runs); re-measured in
+// round 5 on its row shards (`profiles/r05b/ab_grec_shards.txt`): 1/2 (2.26
+// generations) 0.460 -> 0.453 ms, 1/3 (1.51) 0.335 -> 0.322, but 1/4 (1.13)
+// 0.270 -> 0.277; config 2 gains no group
 #ifndef RT_GREC_MIN_GEN
-#define RT_GREC_MIN_GEN 3.0
+#define RT_GREC_MIN_GEN 1.4
 #endif
 bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
     if (K.bvh_nodes || K.max_bounces <= 0) return false;
