@@ -265,6 +265,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_span = ev_start.elapsed_time(ev_end) / args.steps
+    launched = r.last_kernel_name()  # the render kernel the launch policy picked for this rank's work
     t = torch.tensor([elapsed, kern_span, t_issued - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -325,8 +326,10 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         samples = W * H * SPP * MB * args.steps
         value = samples / elapsed / 1e6
-        # roofline of the dominant kernel (the sorted kernel; the BVH refill
-        # kernel for the stress scene), per launch
+        # roofline of the dominant kernel (rank 0's render kernel, as the
+        # library reports it: the sorted kernel on full frames, the pair
+        # kernel on small shards, the BVH refill kernel for the stress
+        # scene), per launch
         units = my_rows * W * SPP  # pixel-passes in one launch on this rank
         alg_bytes = units * BYTES_PER_PIXEL_PASS
         achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
@@ -365,7 +368,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (round(traffic["hbm_bytes_per_launch"]) if traffic else None),
-                         "kernel": "rt_render_bvh_refill_kernel" if scene_key == "stress" else "rt_render_sorted_kernel",
+                         "kernel": launched,
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "bytes_per_unit": BYTES_PER_PIXEL_PASS, "units_per_launch": units},
         }

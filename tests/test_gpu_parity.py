@@ -73,9 +73,11 @@ def test_config3_07_full_size(gpu, oracle):
 # the per-rank workloads of the headline metric's 2 / 4 / 8-GPU points
 # (rank r of G renders rows y = r mod G), plus 6 rows apart, the pair kernel's
 # boundary (345,600 pixels <= 256 CUs x RT_SPREAD_PIX 1,400), each through the
-# DEFAULT launch policy and the kernel it picks for that shard
-@pytest.mark.parametrize("stride,offset,kernel", [(2, 1, "rt_render_sorted_kernel<256"),
-                                                  (4, 3, "rt_render_sorted_kernel<256"),
+# DEFAULT launch policy and the kernel it picks for that shard (global
+# records from RT_GREC_MIN_GEN = 1.4 resident generations: 1/2 has 2.26, 1/4
+# 1.13)
+@pytest.mark.parametrize("stride,offset,kernel", [(2, 1, "rt_render_sorted_kernel<256,grec>"),
+                                                  (4, 3, "rt_render_sorted_kernel<256>"),
                                                   (6, 2, "rt_render_pair_kernel<128>"),
                                                   (8, 5, "rt_render_pair_kernel<128>")])
 def test_config3_shards(gpu, oracle, stride, offset, kernel):
