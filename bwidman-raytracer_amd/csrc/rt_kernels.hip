@@ -1286,6 +1286,13 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     PixelState px;
     load_item(K, npix, nitems, group * BLOCK + tid, px);
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
+#ifdef RT_GTIMES
+    // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g],
+    // [2g+1]; each lane's pixel-done time -> K.stamps[2 * 65536 + 64g + lane]
+    // (tools/gtimes_lanes.py)
+    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    bool gt_done = false;
+#endif
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     int depth = -1;          // -1: the next ray is a camera ray
@@ -1400,6 +1407,11 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             if (depth < 0) {
                 if (px.passes_left <= 0) {
                     idle = true;
+#ifdef RT_GTIMES
+                    if (!gt_done && K.stamps && blockIdx.x < 65536)
+                        K.stamps[2 * 65536 + 64 * (long)blockIdx.x + tid] = __builtin_amdgcn_s_memrealtime();
+                    gt_done = true;
+#endif
                     break;
                 }
                 // jittered camera ray (Main.cu:290-292)
@@ -1505,6 +1517,9 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
         const long g = K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
         K.group_cost[g] = (unsigned)__builtin_amdgcn_s_memrealtime() - K.group_cost[g];
     }
+#ifdef RT_GTIMES
+    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef RT_STAMPS
     if ((threadIdx.x & 63) == 0 && K.stamps)
         for (int k = 0; k < 6; k++) atomicAdd(&K.stamps[k], st_acc[k]);
