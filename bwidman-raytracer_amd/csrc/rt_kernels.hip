@@ -1310,6 +1310,12 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     const float* nodes = K.bvh_nodes;
     const unsigned* nodes16 = K.bvh_nodes16;
     const int nn = K.bvh_n_nodes;
+    // a walk is live while its node indexes the array: -1 (done) and nn (past
+    // a leaf that ends the array: a leaf's miss link is simply node + 1) fail
+    // the same unsigned compare, and the leaf test reuses the decoded flag —
+    // 39 -> 34 VALU per node step: config 5 86.5 -> 85.7 ms, its 1/8 shard
+    // 20.1 -> 19.65 (profiles/r05h/ab_node_step.txt)
+#define NODE_LIVE(n) ((unsigned)(n) < (unsigned)nn)
 #ifdef RT_STAMPS
     // diagnostic: wave cycles in (A) refill, node steps, leaf tests ->
     // K.stamps[0..2]; [3] refill passes, [4] node-loop iterations, [5] leaf batches
@@ -1451,26 +1457,28 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
         while (true) {
             while (true) {  // node steps; a lane parks the first two leaves its ray enters
                 bool stalled = false;
-                if (walking && node >= 0) {
+                if (walking && NODE_LIVE(node)) {
                     RT_BRANCH_COUNT(K, 5);
                     float4 lo, hi;
+                    bool lnode;
                     if (N16) {
-                        const uint4 q = *reinterpret_cast<const uint4*>(nodes16 + 4 * node);
+                        const uint4 q = *reinterpret_cast<const uint4*>(nodes16 + 4u * (unsigned)node);
                         const int w = (int)q.w;
-                        const bool lnode = w < -1;  // a leaf: ~leaf, its miss link is the next node
+                        lnode = w < -1;  // a leaf: ~leaf, its miss link is the next node
                         lo = make_float4(h2f(q.x), h2f(q.x >> 16), h2f(q.y),
-                                         __int_as_float(lnode ? (node + 1 < nn ? node + 1 : -1) : w));
+                                         __int_as_float(lnode ? node + 1 : w));
                         hi = make_float4(h2f(q.y >> 16), h2f(q.z), h2f(q.z >> 16), __int_as_float(lnode ? ~w : -1));
                     } else {
                         lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
                         hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
+                        lnode = __float_as_int(hi.w) >= 0;
                     }
                     const bool hit = slab_enter(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, sr, best_t);
                     const int miss = __float_as_int(lo.w);
                     const int lf = __float_as_int(hi.w);
                     // branch-free step: miss -> skip the subtree; internal -> first
                     // child; leaf -> park it (or stall on a third one)
-                    const bool is_leaf = hit && lf >= 0;
+                    const bool is_leaf = hit && lnode;
                     stalled = is_leaf && leaf2 >= 0;
                     const bool park = is_leaf && leaf2 < 0;
                     leaf2 = park && leaf >= 0 ? lf : leaf2;
@@ -1481,7 +1489,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 // ready (a leaf parked, the walk done or stalled, no walk);
                 // the rest walk on and join a later batch
                 COUNT(4);
-                if (__popcll(__ballot(!walking || leaf >= 0 || node < 0 || stalled)) >= K.leaf_batch) break;
+                if (__popcll(__ballot(!walking || leaf >= 0 || !NODE_LIVE(node) || stalled)) >= K.leaf_batch) break;
             }
             STAMP(1);
             COUNT(5);
@@ -1502,7 +1510,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 leaf2 = -1;
             }
             STAMP(2);
-            if (walking && node < 0) {  // walk complete: the query result is best_t / best_id
+            if (walking && !NODE_LIVE(node)) {  // walk complete: the query result is best_t / best_id
                 walking = false;
                 pending = true;
             }
@@ -1526,6 +1534,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
 #endif
 #undef STAMP
 #undef COUNT
+#undef NODE_LIVE
 }
 #endif  // RT_TU_BVH
 
