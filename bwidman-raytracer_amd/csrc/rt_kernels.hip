@@ -1314,7 +1314,13 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     // a leaf that ends the array: a leaf's miss link is simply node + 1) fail
     // the same unsigned compare, and the leaf test reuses the decoded flag —
     // 39 -> 34 VALU per node step: config 5 86.5 -> 85.7 ms, its 1/8 shard
-    // 20.1 -> 19.65 (profiles/r05h/ab_node_step.txt)
+    // 20.1 -> 19.65 (profiles/r05h/ab_node_step.txt); the 16-byte step below
+    // (one address instruction, ~w parked directly, one compare per parked
+    // leaf) 34 -> 30 VALU, with leaf records loaded in six 16-byte loads
+    // instead of seven (rt_path.h leaf_test): 84.8 -> 84.0 ms, 1/8 shard
+    // 19.64 -> 19.36 (profiles/r05h/ab_node_step3.txt).  Keeping the parked
+    // leaves as loop-carried lane masks (28 VALU) costs more in mask
+    // bookkeeping than it saves: +3 %
 #define NODE_LIVE(n) ((unsigned)(n) < (unsigned)nn)
 #ifdef RT_STAMPS
     // diagnostic: wave cycles in (A) refill, node steps, leaf tests ->
@@ -1459,31 +1465,35 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 bool stalled = false;
                 if (walking && NODE_LIVE(node)) {
                     RT_BRANCH_COUNT(K, 5);
-                    float4 lo, hi;
-                    bool lnode;
-                    if (N16) {
-                        const uint4 q = *reinterpret_cast<const uint4*>(nodes16 + 4u * (unsigned)node);
-                        const int w = (int)q.w;
-                        lnode = w < -1;  // a leaf: ~leaf, its miss link is the next node
-                        lo = make_float4(h2f(q.x), h2f(q.x >> 16), h2f(q.y),
-                                         __int_as_float(lnode ? node + 1 : w));
-                        hi = make_float4(h2f(q.y >> 16), h2f(q.z), h2f(q.z >> 16), __int_as_float(lnode ? ~w : -1));
-                    } else {
-                        lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
-                        hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
-                        lnode = __float_as_int(hi.w) >= 0;
-                    }
-                    const bool hit = slab_enter(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, sr, best_t);
-                    const int miss = __float_as_int(lo.w);
-                    const int lf = __float_as_int(hi.w);
                     // branch-free step: miss -> skip the subtree; internal -> first
                     // child; leaf -> park it (or stall on a third one)
-                    const bool is_leaf = hit && lnode;
-                    stalled = is_leaf && leaf2 >= 0;
-                    const bool park = is_leaf && leaf2 < 0;
-                    leaf2 = park && leaf >= 0 ? lf : leaf2;
-                    leaf = park && leaf < 0 ? lf : leaf;
-                    node = !hit || park ? miss : (is_leaf ? node : node + 1);
+                    if (N16) {
+                        const uint4 q = reinterpret_cast<const uint4*>(nodes16)[(unsigned)node];
+                        const int w = (int)q.w;  // miss link (internal) or ~leaf (a leaf's miss link is node + 1)
+                        const bool lnode = w < -1;
+                        const bool hit = slab_enter(h2f(q.x), h2f(q.x >> 16), h2f(q.y), h2f(q.y >> 16), h2f(q.z),
+                                                    h2f(q.z >> 16), sr, best_t);
+                        const bool is_leaf = hit && lnode;
+                        const bool park = is_leaf && leaf2 < 0;
+                        stalled = is_leaf != park;
+                        const bool first = park && leaf < 0;
+                        leaf2 = park != first ? ~w : leaf2;
+                        leaf = first ? ~w : leaf;
+                        node = !hit && !lnode ? w : (stalled ? node : node + 1);
+                    } else {
+                        const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
+                        const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
+                        const bool hit = slab_enter(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, sr, best_t);
+                        const int miss = __float_as_int(lo.w);
+                        const int lf = __float_as_int(hi.w);
+                        const bool is_leaf = hit && lf >= 0;
+                        const bool park = is_leaf && leaf2 < 0;
+                        stalled = is_leaf != park;
+                        const bool first = park && leaf < 0;
+                        leaf2 = park != first ? lf : leaf2;
+                        leaf = first ? lf : leaf;
+                        node = !hit || park ? miss : (is_leaf ? node : node + 1);
+                    }
                 }
                 // test the parked leaves once K.leaf_batch of the 64 lanes are
                 // ready (a leaf parked, the walk done or stalled, no walk);

@@ -621,6 +621,12 @@ RT_HD void leaf_test(const rt_kparams& K, const float* r, f3 o, f3 d, float a2, 
     if (dot(mk(c2.x, c2.y, c2.z), sub(P, mk(c1.y, c1.z, c1.w))) < 0.0f) return;
     const float4 c3 = *reinterpret_cast<const float4*>(r + 12);  // v1.yz, in1.xy
     const float4 c4 = *reinterpret_cast<const float4*>(r + 16);  // in1.z, v2.xyz
+#if defined(__HIP_DEVICE_COMPILE__)
+    // c4 in one 16-byte load here (edge 2's v2 rides along): otherwise the
+    // compiler loads in1.z alone and v2 again with in2, one more wave-load
+    // of the same line
+    asm volatile("" ::"v"(c4.y), "v"(c4.z), "v"(c4.w));
+#endif
     if (dot(mk(c3.z, c3.w, c4.x), sub(P, mk(c2.w, c3.x, c3.y))) < 0.0f) return;
     const float4 c5 = *reinterpret_cast<const float4*>(r + 20);  // in2.xyz, v3.x
     if (dot(mk(c5.x, c5.y, c5.z), sub(P, mk(c4.y, c4.z, c4.w))) < 0.0f) return;
