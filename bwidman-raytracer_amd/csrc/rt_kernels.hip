@@ -1463,7 +1463,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
         while (true) {
             while (true) {  // node steps; a lane parks the first two leaves its ray enters
                 bool stalled = false;
-                if (walking && NODE_LIVE(node)) {
+                if (NODE_LIVE(node)) {  // (a live node implies a walk)
                     RT_BRANCH_COUNT(K, 5);
                     // branch-free step: miss -> skip the subtree; internal -> first
                     // child; leaf -> park it (or stall on a third one)
@@ -1499,7 +1499,12 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 // ready (a leaf parked, the walk done or stalled, no walk);
                 // the rest walk on and join a later batch
                 COUNT(4);
-                if (__popcll(__ballot(!walking || leaf >= 0 || !NODE_LIVE(node) || stalled)) >= K.leaf_batch) break;
+                // (a lane without a walk has a dead node, and a stalled lane
+                // has a parked leaf; two compare masks OR'd on the scalar
+                // side: a ballot of anything but one compare costs a
+                // v_cndmask + v_cmp per step — config 5 83.9 -> 81.3 ms, its
+                // 1/8 shard 19.2 -> 18.3, profiles/r05h/ab_ballot.txt)
+                if (__popcll(__ballot(leaf >= 0) | __ballot(!NODE_LIVE(node))) >= K.leaf_batch) break;
             }
             STAMP(1);
             COUNT(5);
@@ -1528,7 +1533,9 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             // K.refill of 64 relative to the lanes that still have a pixel, so a
             // wave's tail (pixels done, lanes idle) keeps refilling: config 5
             // 120.4 -> 117.4 ms, its 1/8 shard 26.6 -> 25.6 ms (absolute count)
-            if (w == 0ull || 64 * __popcll(__ballot(!walking && !idle)) >= K.refill * __popcll(__ballot(!idle))) break;
+            // (all 64 lanes are active here: the finished ones are ~w & ~idle)
+            const unsigned long long live = ~__ballot(idle);
+            if (w == 0ull || 64 * __popcll(~w & live) >= K.refill * __popcll(live)) break;
         }
     }
     if (ORDER && tid == 0) {  // the loop exit is wave-uniform (one wave per group)
