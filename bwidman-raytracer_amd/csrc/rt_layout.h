@@ -134,8 +134,11 @@ struct rt_kparams {
 #ifndef RT_LEAF_BATCH_SMALL
 #define RT_LEAF_BATCH_SMALL 62
 #endif
+// (refill 40 on full frames since the round-5 node-step trimming: config 5
+// 80.8 -> 80.1 ms over five alternating pairs; small shards flat between 28
+// and 36, profiles/r05h/ab_refill5.txt)
 #ifndef RT_REFILL
-#define RT_REFILL 36
+#define RT_REFILL 40
 #endif
 #ifndef RT_REFILL_SMALL
 #define RT_REFILL_SMALL 36
