@@ -1,0 +1,32 @@
+"""The benchmark's multi-rank path on the GPU box: a plain
+`python bench.py --gpus 2` starts its own two ranks (torch.distributed.run on
+127.0.0.1), each renders its interleaved-row shard of config 3, the shards
+are gathered and de-interleaved on rank 0, and the gathered frame is checked
+bit for bit against rank 0 rendering the whole frame alone.  With one GPU on
+the box both ranks share it over gloo (BWRT_DIST_BACKEND=gloo); on an 8-GPU
+node the same path runs one rank per GPU over RCCL."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_plain_launch_two_ranks_verified():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(BWRT_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"],
+                       env=env, cwd=REPO, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the one JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["world_size"] == 2 and out["backend"] == "gloo"
+    assert out["verified"] is True, out.get("verify")
+    assert out["value"] > 0 and out["config"]["parallelism"].startswith("pixel-rows/2")
