@@ -596,6 +596,14 @@ RT_HD void leaf_test(const rt_kparams& K, const float* r, f3 o, f3 d, float a2, 
                      int& best_key) {
     const float4 c0 = *reinterpret_cast<const float4*>(r);      // key, n.xyz | key, c.xyz
     const float4 c1 = *reinterpret_cast<const float4*>(r + 4);  // d, v0.xyz   | r^2
+    const float4 c2 = *reinterpret_cast<const float4*>(r + 8);  // in0.xyz, v1.x
+#if defined(__HIP_DEVICE_COMPILE__)
+    // issued with c0 and c1 (the compiler would sink it below the plane
+    // test, one dependent round trip more): config 5 80.9 -> 78.3 ms, its
+    // 1/8 shard 18.4 -> 18.1 (profiles/r05h/ab_hoist.txt); the whole record
+    // up front needs 101 VGPRs (or spills at 96) and gains less
+    asm volatile("" ::"v"(c2.x), "v"(c2.y), "v"(c2.z), "v"(c2.w));
+#endif
     const int key = rt_f2i(c0.x), kind = key & 3, idx = key >> 2;
     if (kind == 0) {  // sphere {c, r^2}, Intersection.cuh:15-62
         const f3 xp = mk(o.x - c0.y, o.y - c0.z, o.z - c0.w);
@@ -612,7 +620,6 @@ RT_HD void leaf_test(const rt_kparams& K, const float* r, f3 o, f3 d, float a2, 
         }
         return;
     }
-    const float4 c2 = *reinterpret_cast<const float4*>(r + 8);  // in0.xyz, v1.x
     const float nd = c0.y * d.x + c0.z * d.y + c0.w * d.z;
     if (fabsf(nd) < RT_NEAR_ZERO) return;
     const float t = -((c0.y * o.x + c0.z * o.y + c0.w * o.z) + c1.x) / nd;
