@@ -140,8 +140,11 @@ struct rt_kparams {
 #ifndef RT_REFILL
 #define RT_REFILL 40
 #endif
+// (small shards: 32 since the round-5 leaf-load change, config 5's 1/8
+// shard 17.86 -> 17.64 ms over two alternating pairs and ahead in the
+// earlier sweep too, profiles/r05h/ab_refill5.txt, ab_knobs6.txt)
 #ifndef RT_REFILL_SMALL
-#define RT_REFILL_SMALL 36
+#define RT_REFILL_SMALL 32
 #endif
 
 // Interleaved test order of Main.cu:221-234 (sphere i, plane i, triangle i,
