@@ -119,7 +119,7 @@ struct rt_context {
     int bvh_nodes_per_order = 0;
     int bvh_order_mask = 7;
     DevBuf scene_buf;  // spheres | planes | triangles | quads | hit table | bvh nodes | bvh prims
-    size_t off_bvh = 0, off_bvh_prims = 0;  // in floats; 0 = no BVH
+    size_t off_bvh = 0, off_bvh_prims = 0, off_bvh_vtx = 0;  // in floats; 0 = no BVH
     size_t off_bvh16 = 0;                   // 16-byte nodes (0 = none: boxes beyond fp16)
     float ovf_sc = 0.0f, ovf_nm = 0.0f, ovf_im = 0.0f;  // overflow bounds (rt_layout.h)
     float cull_dmax = -1.0f;                            // culled rays: max|d_i| bound
@@ -1100,7 +1100,7 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
         if (!(c->cull_dmax > 0.0f)) c->cull_dmax = -1.0f;
     }
     // BVH for large scenes (BWRT_BVH_MIN primitives, default 64)
-    size_t off_bvh = 0, off_bvh_prims = 0, off_bvh16 = 0;
+    size_t off_bvh = 0, off_bvh_prims = 0, off_bvh_vtx = 0, off_bvh16 = 0;
     {
         int bvh_min = 64;
         if (const char* e = tuning_env("BWRT_BVH_MIN")) bvh_min = std::atoi(e);
@@ -1224,8 +1224,12 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             // leaf records, RT_LEAF_FLOATS (128 B) each, and the 16-byte nodes
             // start on 128-byte boundaries: a record spans one cache line
             off_bvh_prims = (off_bvh + B.nodes.size() + 31) & ~(size_t)31;
-            off_bvh16 = B.n16 ? off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS : 0;
-            h.resize(off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS + (B.n16 ? B.nodes16.size() : 0) + 4, 0.0f);
+            // vertex-form leaf records after them (64-byte aligned; the GPU's
+            // ray-refill kernel reads these, the CPU walk the full form), then
+            // the 16-byte nodes
+            off_bvh_vtx = off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS;
+            off_bvh16 = B.n16 ? off_bvh_vtx + B.prims.size() * RT_LEAF_VFLOATS : 0;
+            h.resize(off_bvh_vtx + B.prims.size() * RT_LEAF_VFLOATS + (B.n16 ? B.nodes16.size() : 0) + 4, 0.0f);
             std::memcpy(h.data() + off_bvh, B.nodes.data(), B.nodes.size() * sizeof(float));
             if (B.n16) std::memcpy(h.data() + off_bvh16, B.nodes16.data(), B.nodes16.size() * sizeof(uint32_t));
             for (size_t j = 0; j < B.prims.size(); j++) {
@@ -1246,11 +1250,16 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
                 // the cull sphere wherever the compiled record keeps it
                 const int key = RT_KEY(kind, idx);
                 std::memcpy(&r[0], &key, 4);
+                float* rv = h.data() + off_bvh_vtx + j * RT_LEAF_VFLOATS;  // vertex form
+                std::memcpy(&rv[0], &key, 4);
                 if (kind == 0) {
                     std::memcpy(&r[1], src, (size_t)nf * sizeof(float));
+                    std::memcpy(&rv[1], src, (size_t)nf * sizeof(float));
                 } else {
                     std::memcpy(&r[1], src, 4 * sizeof(float));
                     std::memcpy(&r[5], src + RT_POLY_EDGES, (size_t)(kind == 2 ? 18 : 24) * sizeof(float));
+                    for (int k = 0; k < (kind == 2 ? 3 : 4); k++)
+                        std::memcpy(&rv[1 + 3 * k], src + RT_POLY_EDGES + 6 * k, 3 * sizeof(float));
                 }
             }
         }
@@ -1275,6 +1284,7 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
     c->off_hit = off_hit;
     c->off_bvh = off_bvh;
     c->off_bvh_prims = off_bvh_prims;
+    c->off_bvh_vtx = off_bvh_vtx;
     c->off_bvh16 = tuning_env("BWRT_BVH_N16") && !std::atoi(tuning_env("BWRT_BVH_N16")) ? 0 : off_bvh16;
     c->camera = s->camera;
     c->has_scene = true;
@@ -1535,6 +1545,7 @@ static int prepare(rt_context* c, const rt_render_params* p, rt_kparams& K, unsi
     K.hit = base + c->off_hit;
     K.bvh_nodes = c->off_bvh ? base + c->off_bvh : nullptr;
     K.bvh_leafrec = c->off_bvh ? base + c->off_bvh_prims : nullptr;
+    K.bvh_leafvtx = c->off_bvh ? base + c->off_bvh_vtx : nullptr;
     K.bvh_nodes16 = c->off_bvh && c->off_bvh16 ? reinterpret_cast<const unsigned*>(base + c->off_bvh16) : nullptr;
     K.bvh_n_nodes = c->bvh_nodes_per_order;
     K.ovf_sc = c->ovf_sc;

@@ -1269,8 +1269,16 @@ __device__ __forceinline__ float h2f(unsigned bits) {
 // instead of two; the walk, its tests and its order are the same.
 // ORDER: launch-order feedback as in the sorted kernel (workgroup g renders
 // tile-group group_order[g] and records its duration in group_cost[])
+// Leaf records in vertex form (rt_layout.h bvh_leafvtx: 64 bytes, the plane
+// and inner normals formed in the kernel): config 5 78.6 -> 75.6 ms, 1/2
+// shard 43.0 -> 41.4, 1/8 17.63 -> 17.56 (profiles/r05h/ab_vtx_policy.txt);
+// the kernel held to 5 waves per SIMD (96 VGPRs; 12 bytes of spills on the
+// pixel-load and shading paths)
+#ifndef RT_REFILL_WAVES
+#define RT_REFILL_WAVES 5
+#endif
 template <int BLOCK, bool N16, bool ORDER = false>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU)))
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_REFILL_WAVES)))
 rt_render_bvh_refill_kernel(rt_kparams K) {
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
@@ -1512,16 +1520,16 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 const int first = leaf & 0xffffff, count = leaf >> 24;
                 for (int k = 0; k < count; k++) {
                     RT_BRANCH_COUNT(K, 6);
-                    leaf_test(K, K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
-                              best_key);
+                    leaf_test<true>(K, K.bvh_leafvtx + (size_t)RT_LEAF_VFLOATS * (first + k), o, d, a2, a4, best_t,
+                                    best_id, best_key);
                 }
                 leaf = -1;
             }
             if (leaf2 >= 0) {
                 const int first = leaf2 & 0xffffff, count = leaf2 >> 24;
                 for (int k = 0; k < count; k++)
-                    leaf_test(K, K.bvh_leafrec + (size_t)RT_LEAF_FLOATS * (first + k), o, d, a2, a4, best_t, best_id,
-                              best_key);
+                    leaf_test<true>(K, K.bvh_leafvtx + (size_t)RT_LEAF_VFLOATS * (first + k), o, d, a2, a4, best_t,
+                                    best_id, best_key);
                 leaf2 = -1;
             }
             STAMP(2);
@@ -1695,16 +1703,17 @@ hipError_t rt_launch_render_bvh_refill(const rt_kparams& K0, int num_cus, hipStr
     } else if (K.order_n != grid) {
         K.group_order = nullptr;  // no order for this grid yet: blockIdx order
     }
-    if (feedback && K.bvh_nodes16)
+    const bool n16 = K.bvh_nodes16 != nullptr;
+    if (feedback && n16)
         hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, true, true>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
     else if (feedback)
         hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false, true>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
-    else if (K.bvh_nodes16)
+    else if (n16)
         hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, true>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
     else
         hipLaunchKernelGGL((rt_render_bvh_refill_kernel<BLOCK, false>), dim3((unsigned)grid), dim3(BLOCK), lds, s, K);
     std::snprintf(rt_launched_kernel, sizeof rt_launched_kernel, "rt_render_bvh_refill_kernel<64%s>%s",
-                  K.bvh_nodes16 ? ",n16" : "", feedback ? "+order" : "");
+                  n16 ? ",n16" : "", feedback ? "+order" : "");
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && feedback && (K0.order_sort || K0.order_n != grid)) {
         e = rt_launch_order_groups(K0.group_cost, K0.group_order, grid, s);

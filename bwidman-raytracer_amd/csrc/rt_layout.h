@@ -37,6 +37,7 @@
 #define RT_QUAD_CULL 28
 #define RT_POLY_EDGES 4  // offset of {v0, in0, v1, in1, ...} in a polygon record
 #define RT_LEAF_FLOATS 32  // BVH leaf record: RT_KEY + the record without its cull sphere (<= 28 floats)
+#define RT_LEAF_VFLOATS 16 // BVH leaf record, vertex form: RT_KEY + a sphere's {c, r^2} or a polygon's vertices
 #ifndef RT_HIT_FLOATS
 #define RT_HIT_FLOATS 16
 #endif
@@ -81,6 +82,11 @@ struct rt_kparams {
     // record without its cull sphere}.
     const float* bvh_nodes;
     const float* bvh_leafrec;   // leaf records in leaf order, RT_LEAF_FLOATS each
+    // the same leaves in vertex form (RT_LEAF_VFLOATS each: polygons as
+    // {key, v0, v1, v2[, v3]}, the kernel forms their planes and inner
+    // normals with compile_polygon's own float operations: three loads in
+    // one round trip instead of six in three) — the ray-refill kernel's form
+    const float* bvh_leafvtx;
     int bvh_order_stride;
     int bvh_order_mask;         // octant bits with their own arrays (7 = all three axes)
     // the same arrays as 16-byte nodes (null when a box exceeds the fp16

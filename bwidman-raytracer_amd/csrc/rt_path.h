@@ -592,11 +592,13 @@ RT_HD bool slab_enter(float lx, float ly, float lz, float hx, float hy, float hz
 // trip; config 5 89.8 -> 88.8 ms); each later edge loads only the 16-byte
 // pieces it still needs, so a lane whose point fails an edge requests no
 // further record bytes (the walk is bound by its L1 / L2 request traffic).
+// VTX: the record in vertex form (rt_layout.h bvh_leafvtx)
+template <bool VTX = false>
 RT_HD void leaf_test(const rt_kparams& K, const float* r, f3 o, f3 d, float a2, float a4, float& best_t, int& best_id,
                      int& best_key) {
     const float4 c0 = *reinterpret_cast<const float4*>(r);      // key, n.xyz | key, c.xyz
     const float4 c1 = *reinterpret_cast<const float4*>(r + 4);  // d, v0.xyz   | r^2
-    const float4 c2 = *reinterpret_cast<const float4*>(r + 8);  // in0.xyz, v1.x
+    const float4 c2 = *reinterpret_cast<const float4*>(r + 8);  // in0.xyz, v1.x (RT_LEAF_VERTS: v2.yz, v3.xy)
 #if defined(__HIP_DEVICE_COMPILE__)
     // issued with c0 and c1 (the compiler would sink it below the plane
     // test, one dependent round trip more): config 5 80.9 -> 78.3 ms, its
@@ -618,6 +620,33 @@ RT_HD void leaf_test(const rt_kparams& K, const float* r, f3 o, f3 d, float a2, 
                 best_key = key;
             }
         }
+        return;
+    }
+    if (VTX) {
+        // {key, v0 | v1, v2.x | v2.yz, v3.xy | v3.z}: edges, normal, offset and
+        // inner normals exactly as compile_polygon (rt_context.cpp) forms them
+        const f3 v0 = mk(c0.y, c0.z, c0.w), v1 = mk(c1.x, c1.y, c1.z), v2 = mk(c1.w, c2.x, c2.y);
+        const f3 n = cross(sub(v1, v0), sub(v2, v1));
+        const float dd = -dot(n, v0);
+        const float nd = n.x * d.x + n.y * d.y + n.z * d.z;
+        if (fabsf(nd) < RT_NEAR_ZERO) return;
+        const float t = -((n.x * o.x + n.y * o.y + n.z * o.z) + dd) / nd;
+        if (!key_accept(t, key, best_t, best_key)) return;
+        const f3 P = add(o, scale(t, d));
+        // (the edges formed again where they are needed: fewer live registers)
+        if (dot(cross(n, sub(v1, v0)), sub(P, v0)) < 0.0f) return;
+        if (dot(cross(n, sub(v2, v1)), sub(P, v1)) < 0.0f) return;
+        if (kind == 2) {
+            if (dot(cross(n, sub(v0, v2)), sub(P, v2)) < 0.0f) return;
+        } else {
+            const float4 c3 = *reinterpret_cast<const float4*>(r + 12);  // v3.z
+            const f3 v3 = mk(c2.z, c2.w, c3.x);
+            if (dot(cross(n, sub(v3, v2)), sub(P, v2)) < 0.0f) return;
+            if (dot(cross(n, sub(v0, v3)), sub(P, v3)) < 0.0f) return;
+        }
+        best_t = t;
+        best_id = (kind == 2 ? K.n_sph + K.n_pln : K.n_sph + K.n_pln + K.n_tri) + idx;
+        best_key = key;
         return;
     }
     const float nd = c0.y * d.x + c0.z * d.y + c0.w * d.z;

@@ -273,6 +273,50 @@ def test_bvh_forced_on_small_scenes(gpu, oracle, monkeypatch, name, w, h, spp, m
     same_state(gpu, st)
 
 
+@pytest.mark.parametrize("name,w,h,spp,mb,scale", [("07", 320, 180, 4, 5, 1.0), ("04_box", 320, 180, 4, 5, 1.0),
+                                                    ("stress", 96, 54, 2, 8, 1.0), ("stress", 48, 27, 2, 6, 1e3),
+                                                    ("stress", 96, 54, 2, 6, 1e-4)])
+def test_bvh_vertex_leaf_records(bwrt_lib, oracle, monkeypatch, name, w, h, spp, mb, scale):
+    """The ray-refill kernel's vertex-form leaf records: it forms each
+    polygon's plane and inner normals from the vertices with the compile
+    step's own float operations — bit-exact with the oracle on the pyramid's
+    and the box's shared edges (exact ties; BWRT_BVH_MIN=1 routes them
+    through the BVH), the stress scene, and the stress scene scaled so its
+    secondary rays overflow (1e3) or its boxes sit in the fp16 subnormal
+    range (1e-4)."""
+    from bwrt import Renderer
+    monkeypatch.setenv("BWRT_BVH_MIN", "1")
+    r = Renderer(0, lib=bwrt_lib)
+    try:
+        scene = {"07": scenes.scene_07, "04_box": scenes.scene_04_box, "stress": scenes.stress_scene}[name]()
+        if scale != 1.0:
+            scene = _scaled(scene, scale)
+        img, st = run_pair(r, oracle, scene, w, h, spp, mb)
+        assert_kernel(r, "rt_render_bvh_refill_kernel<64")
+        assert np.array_equal(img, st.rgba)
+        same_state(r, st)
+    finally:
+        r.close()
+
+
+def test_config5_rows_vertex_leaf_records(bwrt_lib):
+    """Config 5's 1/8-shard golden rows (32 spp, 8 bounces) on a fresh
+    context: the oracle's digests."""
+    from bwrt import Renderer
+    r = Renderer(0, lib=bwrt_lib)
+    try:
+        g, smp = _c5_golden("rows15")
+        W, H, spp, mb = g["width"], g["height"], g["spp"], g["max_bounces"]
+        r.set_scene(scenes.stress_scene())
+        r.init_rand(W, H, 5, 8)
+        img, acc = r.render(W, H, spp, mb, first_frame=1, row_offset=5, row_stride=8, want_accum=True)
+        rng, _ = r.get_state(135, W)
+        got = _c5_digests(img[::9], acc[::9], rng[:, ::9])
+        assert got == {k: smp[k] for k in got}, got
+    finally:
+        r.close()
+
+
 @pytest.mark.parametrize("w,h", [(100, 37), (1, 1), (63, 65)])
 def test_ragged_sizes(gpu, oracle, w, h):
     img, st = run_pair(gpu, oracle, scenes.scene_07(), w, h, 3, 4)
