@@ -603,7 +603,8 @@ RT_HD void leaf_test(const rt_kparams& K, const float* r, f3 o, f3 d, float a2, 
     // issued with c0 and c1 (the compiler would sink it below the plane
     // test, one dependent round trip more): config 5 80.9 -> 78.3 ms, its
     // 1/8 shard 18.4 -> 18.1 (profiles/r05h/ab_hoist.txt); the whole record
-    // up front needs 101 VGPRs (or spills at 96) and gains less
+    // up front needs 101 VGPRs (or spills at 96) and gains less.  (The
+    // ray-refill kernel has since read the vertex form, VTX: 76.2 ms.)
     asm volatile("" ::"v"(c2.x), "v"(c2.y), "v"(c2.z), "v"(c2.w));
 #endif
     const int key = rt_f2i(c0.x), kind = key & 3, idx = key >> 2;
