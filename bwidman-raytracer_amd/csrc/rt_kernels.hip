@@ -1277,6 +1277,9 @@ __device__ __forceinline__ float h2f(unsigned bits) {
 #ifndef RT_REFILL_WAVES
 #define RT_REFILL_WAVES 5
 #endif
+#ifndef RT_NODE_PAIR
+#define RT_NODE_PAIR 1
+#endif
 template <int BLOCK, bool N16, bool ORDER = false>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(RT_REFILL_WAVES)))
 rt_render_bvh_refill_kernel(rt_kparams K) {
@@ -1476,18 +1479,38 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                     // branch-free step: miss -> skip the subtree; internal -> first
                     // child; leaf -> park it (or stall on a third one)
                     if (N16) {
-                        const uint4 q = reinterpret_cast<const uint4*>(nodes16)[(unsigned)node];
-                        const int w = (int)q.w;  // miss link (internal) or ~leaf (a leaf's miss link is node + 1)
-                        const bool lnode = w < -1;
-                        const bool hit = slab_enter(h2f(q.x), h2f(q.x >> 16), h2f(q.y), h2f(q.y >> 16), h2f(q.z),
-                                                    h2f(q.z >> 16), sr, best_t);
-                        const bool is_leaf = hit && lnode;
-                        const bool park = is_leaf && leaf2 < 0;
-                        stalled = is_leaf != park;
-                        const bool first = park && leaf < 0;
-                        leaf2 = park != first ? ~w : leaf2;
-                        leaf = first ? ~w : leaf;
-                        node = !hit && !lnode ? w : (stalled ? node : node + 1);
+#define RT_N16_STEP(q)                                                                                        \
+    do {                                                                                                      \
+        const int w = (int)(q).w; /* miss link (internal) or ~leaf (a leaf's miss link is node + 1) */        \
+        const bool lnode = w < -1;                                                                            \
+        const bool hit = slab_enter(h2f((q).x), h2f((q).x >> 16), h2f((q).y), h2f((q).y >> 16), h2f((q).z), \
+                                    h2f((q).z >> 16), sr, best_t);                                            \
+        const bool is_leaf = hit && lnode;                                                                    \
+        const bool park = is_leaf && leaf2 < 0;                                                               \
+        stalled = is_leaf != park;                                                                            \
+        const bool first = park && leaf < 0;                                                                  \
+        leaf2 = park != first ? ~w : leaf2;                                                                   \
+        leaf = first ? ~w : leaf;                                                                             \
+        node = !hit && !lnode ? w : (stalled ? node : node + 1);                                              \
+    } while (0)
+                        const uint4* nq = reinterpret_cast<const uint4*>(nodes16);
+                        const uint4 q = nq[(unsigned)node];
+#if RT_NODE_PAIR
+                        // the next node in array order is loaded with this one:
+                        // a step that moves to node + 1 (an internal hit, a
+                        // parked or missed leaf) takes it without a second
+                        // round trip — config 5 75.9 -> 74.6 ms, its 1/8
+                        // shard flat (profiles/r05h/ab_node_pair.txt); the
+                        // node after it too (node + 2): 80.0 ms
+                        const int node0 = node;
+                        const uint4 q1 = nq[min((unsigned)node + 1u, (unsigned)nn - 1u)];
+                        RT_N16_STEP(q);
+                        asm volatile("" ::"v"(q1.x), "v"(q1.y), "v"(q1.z), "v"(q1.w));
+                        if (node == node0 + 1 && NODE_LIVE(node)) RT_N16_STEP(q1);
+#else
+                        RT_N16_STEP(q);
+#endif
+#undef RT_N16_STEP
                     } else {
                         const float4 lo = *reinterpret_cast<const float4*>(nodes + 8 * node);
                         const float4 hi = *reinterpret_cast<const float4*>(nodes + 8 * node + 4);
