@@ -67,6 +67,9 @@ def parse():
                          "rows (N > 1 always checks the gathered frame against rank 0's single-GPU render)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: gather each frame before the next render starts (no frame pipelining)")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the multi-rank path even at N = 1: process group (RCCL unless BWRT_DIST_BACKEND), "
+                         "rooted gather of the row blocks, de-interleave kernel, verify against a solo render")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
     return ap.parse_args()
@@ -140,14 +143,21 @@ def load_traffic(path, workload_key):
     return None
 
 
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+            "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")
+
+
 def self_launch_command(argv, nproc, port):
     """The command and environment that run this script as `nproc` ranks of
     torch.distributed.run on this node (rendezvous on 127.0.0.1:port), with
     the same arguments; each rank then reads RANK / LOCAL_RANK / WORLD_SIZE."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
-    env = dict(os.environ)
-    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"  # dmabuf IPC: RCCL needs it on this driver
+    # a rank identity left in the caller's environment (this process under
+    # another launcher) must not leak into the children: torch.distributed.run
+    # sets every one of these itself
+    env = {k: v for k, v in os.environ.items() if k not in RANK_ENV}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: RCCL needs it on this driver
     env.setdefault("OMP_NUM_THREADS", "1")  # torch.distributed.run would print a warning and set it
     return cmd, env
 
@@ -160,7 +170,7 @@ def free_port():
 
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.dist) and "WORLD_SIZE" not in os.environ:
         # a plain launch for N GPUs: start the N ranks as children.  Nothing
         # here has touched the GPU (importing torch does not), and this
         # process only waits for them: no exec, no retry
@@ -179,7 +189,10 @@ def main():
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     backend = os.environ.get("BWRT_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
-    if world > 1:
+    # the multi-rank path: every N > 1 run, and N = 1 under --dist (the same
+    # process group, gather, de-interleave and verify with one rank)
+    distributed = world > 1 or args.dist
+    if distributed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -205,13 +218,13 @@ def main():
     # N > 1: frames are pipelined — frame k's gather + de-interleave run on a
     # second stream while frame k+1 renders (double-buffered row blocks);
     # the timed region still covers every render and every gather
-    overlap = world > 1 and not args.no_overlap
+    overlap = distributed and not args.no_overlap
     nbuf = 2 if overlap else 1
     local_imgs = [torch.zeros(rows_per * W, dtype=torch.int32, device=dev) for _ in range(nbuf)]
     full_img = torch.empty(H * W, dtype=torch.int32, device=dev) if rank == 0 else None
     # the gather's landing buffers exist on the root only
     gathered = ([torch.empty((world, rows_per * W), dtype=torch.int32, device=dev) for _ in range(nbuf)]
-                if world > 1 and rank == 0 else [None] * nbuf)
+                if distributed and rank == 0 else [None] * nbuf)
     # the context's own stream (rt_get_stream), wrapped for torch: the
     # kernel, the bench's timing events and the RCCL gather are all ordered
     # on it, and renders on the context's stream defer the library's end
@@ -232,9 +245,9 @@ def main():
         local_img = local_imgs[b]
         if overlap:
             stream.wait_event(ev_sent[b])  # no-op until the event is first recorded
-        r.render_device(params, local_img.data_ptr() if world > 1 else full_img.data_ptr(),
+        r.render_device(params, local_img.data_ptr() if distributed else full_img.data_ptr(),
                         stream.cuda_stream)
-        if world > 1:
+        if distributed:
             ev_rendered[b].record(stream)
             with torch.cuda.stream(comm):
                 comm.wait_event(ev_rendered[b])
@@ -251,7 +264,7 @@ def main():
     # the launches); the average launch = their span / K, which also covers
     # the order-sort kernel and the launch gaps of each step
     ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -261,17 +274,17 @@ def main():
     ev_end.record(stream)
     t_issued = time.perf_counter()  # host time to enqueue the steps (must stay below the GPU time)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_span = ev_start.elapsed_time(ev_end) / args.steps
     launched = r.last_kernel_name()  # the render kernel the launch policy picked for this rank's work
     t = torch.tensor([elapsed, kern_span, t_issued - t0], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_avg_ms, issue_s = float(t[0]), float(t[1]), float(t[2])
     kernel_timing = "event pair around the timed launches on the render stream, / steps"
-    if world > 1:
+    if distributed:
         # the timed region's span on the render stream also holds its waits
         # for the gather stream (and, with --no-overlap, the gather itself):
         # the render kernel's own time comes from render-only launches after
@@ -293,7 +306,7 @@ def main():
     # from fresh seeds against rank 0 rendering the whole frame alone); N = 1
     # with --verify (a fresh frame against the CPU fallback on a row sample)
     verified, verify_how = None, None
-    if world > 1:
+    if distributed:
         r.init_rand(W, H, plan.row_offset, plan.row_stride)
         step()
         torch.cuda.synchronize(dev)
@@ -351,10 +364,10 @@ def main():
             "config": {"workload": f"07_specular_BRDF {W}x{H} {SPP}spp {MB}-bounce (BASELINE configs[2])"
                        if args.config == "c3" else f"{args.config}: scene {scene_key} {W}x{H} {SPP}spp {MB}-bounce",
                        "scene": scene_key, "width": W, "height": H, "spp": SPP, "max_bounces": MB,
-                       "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} gather" if world > 1 else "")
+                       "parallelism": f"pixel-rows/{world}" + (f" + {'rccl' if backend == 'nccl' else backend} gather" if distributed else "")
                        + (" (frames pipelined: gather of frame k overlaps render of k+1)" if overlap else "")},
             "world_size": world,
-            "backend": (("rccl" if backend == "nccl" else backend) if world > 1 else None),
+            "backend": (("rccl" if backend == "nccl" else backend) if distributed else None),
             "verified": verified,
             "verify": verify_how,
             "ms_per_frame": round(ms_step, 4),
@@ -386,7 +399,7 @@ def main():
                 "issue_frac": round(v["insts_valu_per_launch"] / ks / inst_peak, 4),
                 "active_lanes_per_valu": round(v["active_lanes_per_valu"], 2),
                 "counters": traffic.get("source")}
-        if world == 1 and not args.no_cpu_baseline:
+        if not distributed and not args.no_cpu_baseline:
             torch.cuda.synchronize(dev)
             with Renderer(dev_index, lib=lib) as check:
                 check.set_scene(scene)
@@ -397,12 +410,12 @@ def main():
                 out["verify"] = "the CPU baseline's sample: GPU vs the CPU fallback from the same seeds, bit for bit"
         print(json.dumps(out), flush=True)
     ok = torch.tensor([0 if verified is False else 1], dtype=torch.int32, device=dev)
-    if world > 1:
+    if distributed:
         dist.broadcast(ok, 0)
     torch.cuda.synchronize(dev)
     torch.cuda.set_stream(torch.cuda.default_stream(dev))  # the context's stream goes with it
     r.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     if int(ok[0]) == 0 or (rank == 0 and world == 1 and out.get("verified") is False):
         print("verify FAILED: the measured path's frame differs", file=sys.stderr, flush=True)

@@ -29,7 +29,7 @@
 #include "rt_layout.h"
 
 size_t rt_render_rec_floats(const rt_kparams& K);
-bool rt_render_wants_global_records(const rt_kparams& K, int num_cus);
+int rt_render_global_records(const rt_kparams& K, int num_cus, int req);
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
                             hipStream_t stream, int pair_req);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
@@ -147,7 +147,7 @@ struct rt_context {
     bool order_stale = true;
     unsigned long long launches = 0;
     bool order_feedback = true;  // BWRT_ORDER=0: blockIdx order
-    int grec = -1;  // BWRT_GREC: 1 / 0 force global / LDS records; -1 = launch policy
+    int grec = -1;  // BWRT_GREC: 1 / 2 / 0 force global records (7-wave / 8-wave shape) / LDS records; -1 = policy
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
     size_t host_rgba_bytes = 0;
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
@@ -905,7 +905,7 @@ int rt_create(int device, rt_context** out) {
         if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
     }
     if (const char* g = tuning_env("BWRT_TILE_SQ")) c->tile_sq = std::atoi(g) != 0;
-    if (const char* g = tuning_env("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
+    if (const char* g = tuning_env("BWRT_GREC")) c->grec = std::atoi(g) == 2 ? 2 : std::atoi(g) ? 1 : 0;
     if (const char* g = tuning_env("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = tuning_env("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = tuning_env("BWRT_SPREAD")) c->spread = std::atoi(g) ? 1 : 0;
@@ -1221,15 +1221,16 @@ int rt_set_scene(rt_context* c, const rt_scene* s) {
             c->bvh_nodes_per_order = B.n_nodes;
             c->bvh_order_mask = B.order_mask;
             off_bvh = (total + 3) & ~(size_t)3;
-            // leaf records, RT_LEAF_FLOATS (128 B) each, and the 16-byte nodes
-            // start on 128-byte boundaries: a record spans one cache line
+            // leaf records, RT_LEAF_FLOATS (128 B) each, start on a 128-byte
+            // boundary: a record spans one cache line
             off_bvh_prims = (off_bvh + B.nodes.size() + 31) & ~(size_t)31;
-            // vertex-form leaf records after them (64-byte aligned; the GPU's
-            // ray-refill kernel reads these, the CPU walk the full form), then
-            // the 16-byte nodes
+            // vertex-form leaf records after them (64 B each, 64-byte aligned;
+            // the GPU's ray-refill kernel reads these, the CPU walk the full
+            // form), then the 16-byte nodes, again from a 128-byte boundary
+            // (eight nodes per line, the same lines for every scene)
             off_bvh_vtx = off_bvh_prims + B.prims.size() * RT_LEAF_FLOATS;
-            off_bvh16 = B.n16 ? off_bvh_vtx + B.prims.size() * RT_LEAF_VFLOATS : 0;
-            h.resize(off_bvh_vtx + B.prims.size() * RT_LEAF_VFLOATS + (B.n16 ? B.nodes16.size() : 0) + 4, 0.0f);
+            off_bvh16 = B.n16 ? (off_bvh_vtx + B.prims.size() * RT_LEAF_VFLOATS + 31) & ~(size_t)31 : 0;
+            h.resize((B.n16 ? off_bvh16 + B.nodes16.size() : off_bvh_vtx + B.prims.size() * RT_LEAF_VFLOATS) + 4, 0.0f);
             std::memcpy(h.data() + off_bvh, B.nodes.data(), B.nodes.size() * sizeof(float));
             if (B.n16) std::memcpy(h.data() + off_bvh16, B.nodes16.data(), B.nodes16.size() * sizeof(uint32_t));
             for (size_t j = 0; j < B.prims.size(); j++) {
@@ -1597,7 +1598,8 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     K.refill = c->refill > 0 ? c->refill : small ? RT_REFILL_SMALL : RT_REFILL;
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
-    if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K, c->num_cus)))) {
+    K.grec_mode = c->simple ? 0 : rt_render_global_records(K, c->num_cus, c->grec);
+    if (K.grec_mode) {
         const int rc = ensure_buf(c, c->rec, rt_render_rec_floats(K) * sizeof(float));
         if (rc) return rc;
         K.rec = (float*)c->rec.p;
@@ -1610,7 +1612,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
         K.stamps = stamps;
     }
     const char* gtimes = tuning_env("BWRT_GTIMES");  // diagnostic builds (-DRT_GTIMES): group times file
-    const size_t NGT = (size_t)1 << 22;
+    const size_t NGT = (size_t)RT_GTIMES_WORDS;
     if (gtimes && !stamps) {
         if (hipMalloc(&stamps, NGT * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemsetAsync(stamps, 0, NGT * sizeof(unsigned long long), s);

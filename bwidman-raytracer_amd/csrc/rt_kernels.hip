@@ -33,6 +33,7 @@
 
 #include <cstdio>
 
+#include "rt_diag.h"
 #include "rt_layout.h"
 #include "rt_path.h"
 
@@ -208,32 +209,6 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
                                           __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
 
-// ---- diagnostics: RT_PHASE_TWICE = 1 / 2 / 3 / 4 runs the sorted kernel's
-// closest hit / RANDDIR task / SPEC task / path-end fold a second time on
-// opaque copies of its inputs (results kept alive, never used), so the PMC
-// deltas against the plain build (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU) are
-// that phase's VALU instructions and lane-cycles (tools/phase_lanes.sh)
-#ifndef RT_PHASE_TWICE
-#define RT_PHASE_TWICE 0
-#endif
-__device__ __forceinline__ float opq(float x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ f3 opq3(f3 v) { return mk(opq(v.x), opq(v.y), opq(v.z)); }
-__device__ __forceinline__ void keep(float x) { asm volatile("" ::"v"(x)); }
-__device__ __forceinline__ void keep_i(int x) { asm volatile("" ::"v"(x)); }
-__device__ __forceinline__ Xorwow opq_rs(Xorwow r) {
-    Xorwow q;
-    q.d = __float_as_uint(opq(__uint_as_float(r.d)));
-    q.v0 = __float_as_uint(opq(__uint_as_float(r.v0)));
-    q.v1 = __float_as_uint(opq(__uint_as_float(r.v1)));
-    q.v2 = __float_as_uint(opq(__uint_as_float(r.v2)));
-    q.v3 = __float_as_uint(opq(__uint_as_float(r.v3)));
-    q.v4 = __float_as_uint(opq(__uint_as_float(r.v4)));
-    return q;
-}
-
 // RT_KEY of a primitive id (spheres, planes, triangles, quads in turn); -1 for -1
 __device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
     const int e_pln = K.n_sph, e_tri = e_pln + K.n_pln, e_quad = e_tri + K.n_tri;
@@ -271,6 +246,15 @@ __device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
 #ifndef RT_GREC_LDS_LEVELS
 #define RT_GREC_LDS_LEVELS 2
 #endif
+// global-record shapes (template GREC of the sorted kernel, K.grec_mode):
+// 0 = the record stack in LDS; 1 = RT_GREC_LDS_LEVELS shallow levels in LDS
+// at RT_GREC_WAVES waves per SIMD (full frames, deep paths); 2 = one LDS
+// level at 8 waves per SIMD (64 VGPRs): 8 groups of 256 lanes per CU, for
+// frames and shards that fit one resident generation of it
+__host__ __device__ constexpr int grec_lds_levels(int mode) { return mode == 2 ? 1 : RT_GREC_LDS_LEVELS; }
+__host__ __device__ constexpr int sorted_waves_per_eu(int mode) {
+    return mode == 2 ? 8 : mode ? RT_GREC_WAVES : RT_WAVES_PER_EU;
+}
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
 #endif
@@ -527,8 +511,8 @@ enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };  // a lane's next task
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
 // GREC: the record levels >= RT_GREC_LDS_LEVELS in global memory (deep paths
 // and full frames, launch policy).  BVH scenes take the ray-refill kernel.
-template <int BLOCK, bool HIT_LDS, bool GREC, bool ORDER = false, bool QUADS = true>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
+template <int BLOCK, bool HIT_LDS, int GREC, bool ORDER = false, bool QUADS = true>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(sorted_waves_per_eu(GREC))))
 rt_render_sorted_kernel(rt_kparams K) {
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
@@ -551,7 +535,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     // reached) in global memory, [group][level - LL][field][lane] (each
     // group's records contiguous and coalesced), so LDS leaves room for
     // RT_GREC_WAVES waves and few records ever leave the CU
-    const int LL = GREC ? (levels < RT_GREC_LDS_LEVELS ? levels : RT_GREC_LDS_LEVELS) : levels;
+    const int LL = GREC ? (levels < grec_lds_levels(GREC) ? levels : grec_lds_levels(GREC)) : levels;
     // (an LDS-address-space pointer: 32-bit address arithmetic, no 64-bit
     // base held across the loop)
     lds_float* rec = (lds_float*)(rec_base + tid);
@@ -563,10 +547,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
     if (tid < 4) counters[tid] = 0;
-#ifdef RT_GTIMES
-    // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g], [2g+1]
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
+    diag_group_start(K);
     __syncthreads();
 #define SLOT(f, i) slots[(f) * BLOCK + (i)]
 // task results {r.xyz, kspec, rng[6]}, written back over the slot's own
@@ -596,36 +577,25 @@ rt_render_sorted_kernel(rt_kparams K) {
 
     // path end: fold, accumulate (Main.cu:299-304), next frame / next pixel
     auto finish_path = [&](int slot) {
-        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
-        if (depth > K.max_bounces)  // deepest level, parked in the slot
-            fold_level(__float_as_int(SLOT(6, slot)), SLOT(4, slot), SLOT(5, slot), hit_tab, lx, ly, lz);
-        const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
-        if (GREC)
-            for (int l = nrec - 1; l >= LL; --l) {
-                const float* r = grec + 3 * (l - LL) * BLOCK;
-                fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
-            }
-        for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
-            const lds_float* r = rec + 3 * l * BLOCK;
-            fold_level(__float_as_int(r[0]), r[BLOCK], r[2 * BLOCK], hit_tab, lx, ly, lz);
-        }
-#if RT_PHASE_TWICE == 4
-        {
-            float mx = opq(K.bg[0]), my = opq(K.bg[1]), mz = opq(K.bg[2]);
-            if (depth > K.max_bounces)
-                fold_level(__float_as_int(opq(SLOT(6, slot))), opq(SLOT(4, slot)), opq(SLOT(5, slot)), hit_tab, mx, my, mz);
+        // L = emitted + (brdf * L) * cosAngle, innermost level first; `x`
+        // reads each record value (identity; opaque in RT_PHASE_TWICE == 4)
+        auto fold_path = [&](auto x, float& lx, float& ly, float& lz) {
+            if (depth > K.max_bounces)  // deepest level, parked in the slot
+                fold_level(__float_as_int(x(SLOT(6, slot))), x(SLOT(4, slot)), x(SLOT(5, slot)), hit_tab, lx, ly, lz);
+            const int nrec = depth > K.max_bounces ? K.max_bounces : depth;
             if (GREC)
                 for (int l = nrec - 1; l >= LL; --l) {
                     const float* r = grec + 3 * (l - LL) * BLOCK;
-                    fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
+                    fold_level(__float_as_int(x(r[0])), x(r[BLOCK]), x(r[2 * BLOCK]), hit_tab, lx, ly, lz);
                 }
             for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
                 const lds_float* r = rec + 3 * l * BLOCK;
-                fold_level(__float_as_int(opq(r[0])), opq(r[BLOCK]), opq(r[2 * BLOCK]), hit_tab, mx, my, mz);
+                fold_level(__float_as_int(x(r[0])), x(r[BLOCK]), x(r[2 * BLOCK]), hit_tab, lx, ly, lz);
             }
-            keep(mx + my + mz);
-        }
-#endif
+        };
+        float lx = K.bg[0], ly = K.bg[1], lz = K.bg[2];  // backgroundColor (Main.cu:209-211)
+        fold_path(DiagIdent(), lx, ly, lz);
+        RT_TWICE_FOLD(K, fold_path);
         if (px.frame == 1u) {
             px.ax = 0.0f;
             px.ay = 0.0f;
@@ -643,40 +613,14 @@ rt_render_sorted_kernel(rt_kparams K) {
     };
     bool ended = false;  // path ended this round: finish_path() once, after the I-phase
 
-#ifdef RT_STAMPS
-    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define STAMP(k)                                              \
-    do {                                                      \
-        unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-        st_acc[k] += _t - st_prev;                            \
-        st_prev = _t;                                         \
-    } while (0)
-    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
-    // utilisation counters (wave-level, lane 0 adds): [0] rounds, [1] front
-    // waves, [2] front tasks, [3] rejection-loop wave trips, [4] rejection
-    // lane trips, [5] spec waves, [6] spec tasks, [7] I-phase waves,
-    // [8] I-phase rays
-    unsigned long long st_u[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    auto wave_max = [](int v) {
-        for (int m = 1; m < 64; m <<= 1) v = max(v, __shfl_xor(v, m));
-        return v;
-    };
-    auto wave_sum = [](int v) {
-        for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
-        return v;
-    };
-#else
-#define STAMP(k) \
-    do {         \
-    } while (0)
-#endif
+    SortedStamps dg;  // diagnostic builds only (rt_diag.h)
     while (true) {
         const int task = mode;
-        STAMP(7);
+        dg.stamp(7);
         // every owner has read its previous task result out of the slots
         // before any wave overwrites them with this round's tasks
         __syncthreads();
-        STAMP(0);
+        dg.stamp(0);
 
         // ---- T-phase: enqueue (front: RANDDIR, back: SPEC)
         int* cnt = counters + 2 * parity;
@@ -710,9 +654,9 @@ rt_render_sorted_kernel(rt_kparams K) {
             SLOT(11, slot) = __uint_as_float(px.rs.v3);
             SLOT(12, slot) = __uint_as_float(px.rs.v4);
         }
-        STAMP(1);
+        dg.stamp(1);
         __syncthreads();
-        STAMP(2);
+        dg.stamp(2);
         // no task anywhere in the workgroup: every lane is idle (rays are
         // always consumed in the round that made them), so the group is done
         const int nf = cnt[0], nb = cnt[1];
@@ -728,9 +672,6 @@ rt_render_sorted_kernel(rt_kparams K) {
             const bool spec_wave = wave_first + 63 >= BLOCK - nb;
             if (spec_wave) __builtin_amdgcn_s_setprio(RT_SPEC_PRIO);
 #endif
-#ifdef RT_STAMPS
-            int rej_it = 0;
-#endif
             if (do_front || do_spec) {
                 Xorwow rs;
                 rs.d = __float_as_uint(SLOT(7, tid));
@@ -742,35 +683,15 @@ rt_render_sorted_kernel(rt_kparams K) {
                 const f3 nrm = mk(SLOT(0, tid), SLOT(1, tid), SLOT(2, tid));
                 const int code = __float_as_int(SLOT(6, tid));
                 f3 r;
-#ifdef RT_STAMPS
-                int* rej_ptr = &rej_it;
-#else
-                int* rej_ptr = nullptr;
-#endif
                 if (do_front) {
-#if RT_PHASE_TWICE == 2
-                    {
-                        Xorwow r2 = opq_rs(rs);
-                        const f3 x = random_direction(r2, opq3(nrm));
-                        keep(x.x + x.y + x.z);
-                        keep_i((int)r2.v4);
-                    }
-#endif
-                    r = random_direction(rs, nrm, rej_ptr);
+                    RT_TWICE_RANDDIR(rs, nrm);
+                    r = random_direction(rs, nrm, dg.rej_ptr());
                     if (code < 0) r = normalize3(add(nrm, scale(K.jitter, r)));  // camera jitter, Main.cu:291-292
                 } else {
                     const f3 dd = mk(SLOT(3, tid), SLOT(4, tid), SLOT(5, tid));
                     const float4 h2 = *reinterpret_cast<const float4*>(hit_tab + RT_HIT_FLOATS * code + 8);
                     float kspec;
-#if RT_PHASE_TWICE == 3
-                    {
-                        Xorwow r2 = opq_rs(rs);
-                        float k2;
-                        const f3 x = specular_scatter(r2, opq3(dd), opq3(nrm), opq(h2.x), opq(h2.z), opq(h2.y), k2);
-                        keep(x.x + x.y + x.z + k2);
-                        keep_i((int)r2.v4);
-                    }
-#endif
+                    RT_TWICE_SPEC(rs, dd, nrm, h2);
                     r = specular_scatter(rs, dd, nrm, h2.x, h2.z, h2.y, kspec);
                     RES(3, tid) = kspec;
                 }
@@ -784,29 +705,14 @@ rt_render_sorted_kernel(rt_kparams K) {
                 RES(8, tid) = __uint_as_float(rs.v3);
                 RES(9, tid) = __uint_as_float(rs.v4);
             }
-#ifdef RT_STAMPS
-            {
-                const int itl = (do_front && !do_spec) ? rej_it : 0;
-                const unsigned long long bf = __ballot(do_front), bs = __ballot(do_spec);
-                const int mx = wave_max(itl), sm = wave_sum(itl);
-                if (lane == 0) {
-                    st_u[0] += 1;
-                    st_u[1] += bf != 0;
-                    st_u[2] += __popcll(bf);
-                    st_u[3] += mx;
-                    st_u[4] += sm;
-                    st_u[5] += bs != 0;
-                    st_u[6] += __popcll(bs);
-                }
-            }
-#endif
+            dg.exec(do_front, do_spec);
         }
-        STAMP(3);
+        dg.stamp(3);
 #if RT_SPEC_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
         __syncthreads();
-        STAMP(4);
+        dg.stamp(4);
         if (tid == 0) {
             counters[2 * (parity ^ 1)] = 0;
             counters[2 * (parity ^ 1) + 1] = 0;
@@ -856,29 +762,13 @@ rt_render_sorted_kernel(rt_kparams K) {
             }
         }
 
-        STAMP(5);
-#ifdef RT_STAMPS
-        {
-            const unsigned long long br = __ballot(has_ray);
-            if (lane == 0) {
-                st_u[7] += br != 0;
-                st_u[8] += __popcll(br);
-            }
-        }
-#endif
+        dg.stamp(5);
+        dg.rays(has_ray);
         // ---- I-phase: closest hit + brdfChoice (Main.cu:214-245)
         float t = INFINITY;
         int id = -1;
         if (has_ray) {
-#if RT_PHASE_TWICE == 1
-            {
-                float t2;
-                int id2;
-                closest_hit_brute<QUADS>(K, opq3(o), opq3(d), t2, id2);
-                keep(t2);
-                keep_i(id2);
-            }
-#endif
+            RT_TWICE_HIT(QUADS, K, o, d);
             closest_hit_brute<QUADS>(K, o, d, t, id);
         }
         if (has_ray) {
@@ -899,7 +789,7 @@ rt_render_sorted_kernel(rt_kparams K) {
             ended = false;
             finish_path(slot);
         }
-        STAMP(6);
+        dg.stamp(6);
     }
     if (px.valid && px.passes_left == 0 && px.frame != K.first_frame) store_pixel(K, npix, px);
     // the loop exit is group-uniform (the round that posts no task), so one
@@ -914,17 +804,8 @@ rt_render_sorted_kernel(rt_kparams K) {
         const long g = ord ? (long)__builtin_nontemporal_load(&ord[blockIdx.x]) : (long)blockIdx.x;
         cost[g] = (unsigned)__builtin_amdgcn_s_memrealtime() - cost[g];
     }
-#ifdef RT_GTIMES
-    __syncthreads();
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef RT_STAMPS
-    if ((threadIdx.x & 63) == 0 && K.stamps) {
-        for (int k = 0; k < 8; k++) atomicAdd(&K.stamps[k], st_acc[k]);
-        for (int k = 0; k < 9; k++) atomicAdd(&K.stamps[8 + k], st_u[k]);
-    }
-#endif
-#undef STAMP
+    diag_group_end<true>(K);
+    dg.flush(K);
 #undef SLOT
 #undef RES
 }
@@ -982,9 +863,7 @@ rt_render_pair_kernel(rt_kparams K) {
     int* live_flag = reinterpret_cast<int*>(rec_base + 3 * levels * 64 + RT_PAIR_FIELDS * 64);
     const long npix = (long)K.rows * K.width;
     const long nitems = items_of(K, npix);
-#ifdef RT_GTIMES
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
+    diag_group_start(K);
     const long group = ORDER && K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
     if (ORDER && tid == 0) K.group_cost[group] = (unsigned)__builtin_amdgcn_s_memrealtime();
     PixelState px;
@@ -1233,10 +1112,7 @@ rt_render_pair_kernel(rt_kparams K) {
         const long g = ord ? (long)__builtin_nontemporal_load(&ord[blockIdx.x]) : (long)blockIdx.x;
         cost[g] = (unsigned)__builtin_amdgcn_s_memrealtime() - cost[g];
     }
-#ifdef RT_GTIMES
-    __syncthreads();
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
+    diag_group_end<true>(K);
 }
 
 #ifdef RT_TU_BVH
@@ -1297,13 +1173,8 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     PixelState px;
     load_item(K, npix, nitems, group * BLOCK + tid, px);
     const f3 cam = mk(K.cam_pos[0], K.cam_pos[1], K.cam_pos[2]);
-#ifdef RT_GTIMES
-    // diagnostic: per-group start / end (100 MHz realtime) -> K.stamps[2g],
-    // [2g+1]; each lane's pixel-done time -> K.stamps[2 * 65536 + 64g + lane]
-    // (tools/gtimes_lanes.py)
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    bool gt_done = false;
-#endif
+    diag_group_start(K);
+    LaneDone lane_done;  // diagnostic builds only (rt_diag.h)
 
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     int depth = -1;          // -1: the next ray is a camera ray
@@ -1333,53 +1204,14 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
     // leaves as loop-carried lane masks (28 VALU) costs more in mask
     // bookkeeping than it saves: +3 %
 #define NODE_LIVE(n) ((unsigned)(n) < (unsigned)nn)
-#ifdef RT_STAMPS
-    // diagnostic: wave cycles in (A) refill, node steps, leaf tests ->
-    // K.stamps[0..2]; [3] refill passes, [4] node-loop iterations, [5] leaf batches
-    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0};
-    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
-#define STAMP(k)                                              \
-    do {                                                      \
-        unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-        st_acc[k] += _t - st_prev;                            \
-        st_prev = _t;                                         \
-    } while (0)
-#define COUNT(k) (st_acc[k] += 1)
-#else
-#define STAMP(k) \
-    do {         \
-    } while (0)
-#define COUNT(k) \
-    do {         \
-    } while (0)
-#endif
-
+    RefillStamps dg;  // diagnostic builds only (rt_diag.h)
     while (true) {
-        COUNT(3);
+        dg.count(3);
         // (A) lanes without a walk: shade the finished query, start the next ray
         while (!walking && !idle) {
             if (pending) {
                 pending = false;
-#ifdef RT_BVH_CHECK
-                // diagnostic build: the brute-force loop on the same ray; a
-                // disagreement is logged to K.stamps (BWRT_GTIMES buffer):
-                // [0] count, then 16 words per record
-                {
-                    float bt;
-                    int bi;
-                    closest_hit_brute(K, o, d, bt, bi);
-                    if ((bi != best_id || (bi >= 0 && bt != best_t && !(bt != bt && best_t != best_t))) && K.stamps) {
-                        const unsigned long long k = atomicAdd(&K.stamps[0], 1ull);
-                        if (k < 4096) {
-                            unsigned long long* rec = K.stamps + 16 + 16 * k;
-                            rec[0] = __float_as_uint(o.x); rec[1] = __float_as_uint(o.y); rec[2] = __float_as_uint(o.z);
-                            rec[3] = __float_as_uint(d.x); rec[4] = __float_as_uint(d.y); rec[5] = __float_as_uint(d.z);
-                            rec[6] = __float_as_uint(best_t); rec[7] = (unsigned)best_id;
-                            rec[8] = __float_as_uint(bt); rec[9] = (unsigned)bi; rec[10] = (unsigned)depth;
-                        }
-                    }
-                }
-#endif
+                diag_bvh_check(K, o, d, best_t, best_id, depth);
                 bool finished = true;
                 if (best_id >= 0) {  // shade (Main.cu:237-264), as rt_render_kernel
                     const float* h = hit_tab + RT_HIT_FLOATS * best_id;
@@ -1430,11 +1262,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             if (depth < 0) {
                 if (px.passes_left <= 0) {
                     idle = true;
-#ifdef RT_GTIMES
-                    if (!gt_done && K.stamps && blockIdx.x < 65536)
-                        K.stamps[2 * 65536 + 64 * (long)blockIdx.x + tid] = __builtin_amdgcn_s_memrealtime();
-                    gt_done = true;
-#endif
+                    lane_done.mark(K);
                     break;
                 }
                 // jittered camera ray (Main.cu:290-292)
@@ -1467,7 +1295,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
             leaf2 = -1;
             walking = true;
         }
-        STAMP(0);
+        dg.stamp(0);
         if (__ballot(walking) == 0ull) break;  // every lane idle
 
         // (B) walk until K.refill lanes are waiting for a new ray
@@ -1529,7 +1357,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 // test the parked leaves once K.leaf_batch of the 64 lanes are
                 // ready (a leaf parked, the walk done or stalled, no walk);
                 // the rest walk on and join a later batch
-                COUNT(4);
+                dg.count(4);
                 // (a lane without a walk has a dead node, and a stalled lane
                 // has a parked leaf; two compare masks OR'd on the scalar
                 // side: a ballot of anything but one compare costs a
@@ -1537,8 +1365,8 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                 // 1/8 shard 19.2 -> 18.3, profiles/r05h/ab_ballot.txt)
                 if (__popcll(__ballot(leaf >= 0) | __ballot(!NODE_LIVE(node))) >= K.leaf_batch) break;
             }
-            STAMP(1);
-            COUNT(5);
+            dg.stamp(1);
+            dg.count(5);
             if (leaf >= 0) {
                 const int first = leaf & 0xffffff, count = leaf >> 24;
                 for (int k = 0; k < count; k++) {
@@ -1555,7 +1383,7 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
                                     best_id, best_key);
                 leaf2 = -1;
             }
-            STAMP(2);
+            dg.stamp(2);
             if (walking && !NODE_LIVE(node)) {  // walk complete: the query result is best_t / best_id
                 walking = false;
                 pending = true;
@@ -1573,15 +1401,8 @@ rt_render_bvh_refill_kernel(rt_kparams K) {
         const long g = K.group_order ? (long)K.group_order[blockIdx.x] : (long)blockIdx.x;
         K.group_cost[g] = (unsigned)__builtin_amdgcn_s_memrealtime() - K.group_cost[g];
     }
-#ifdef RT_GTIMES
-    if (tid == 0 && K.stamps) K.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef RT_STAMPS
-    if ((threadIdx.x & 63) == 0 && K.stamps)
-        for (int k = 0; k < 6; k++) atomicAdd(&K.stamps[k], st_acc[k]);
-#endif
-#undef STAMP
-#undef COUNT
+    diag_group_end<false>(K);
+    dg.flush(K);
 #undef NODE_LIVE
 }
 #endif  // RT_TU_BVH
@@ -1608,7 +1429,7 @@ namespace {
 // and shards: 128 lanes for 64 pixels)
 enum { K_SIMPLE = 0, K_SORTED = 1, K_PAIR = 2 };
 
-template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, bool GREC = false, bool ORDER = false, bool QUADS = true>
+template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, int GREC = 0, bool ORDER = false, bool QUADS = true>
 void* kernel_ptr() {
     if constexpr (KIND == K_PAIR) return reinterpret_cast<void*>(&rt_render_pair_kernel<HIT_LDS, ORDER, QUADS>);
     if constexpr (KIND == K_SORTED)
@@ -1616,7 +1437,7 @@ void* kernel_ptr() {
     return reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
 }
 
-template <int KIND, int BLOCK, bool HIT_LDS, bool GREC, bool ORDER, bool QUADS>
+template <int KIND, int BLOCK, bool HIT_LDS, int GREC, bool ORDER, bool QUADS>
 void launch_kind(const rt_kparams& K, long grid, size_t lds, hipStream_t stream) {
     if constexpr (KIND == K_PAIR)
         hipLaunchKernelGGL((rt_render_pair_kernel<HIT_LDS, ORDER, QUADS>), dim3((unsigned)grid), dim3(128), lds, stream, K);
@@ -1625,7 +1446,7 @@ void launch_kind(const rt_kparams& K, long grid, size_t lds, hipStream_t stream)
                            dim3(BLOCK), lds, stream, K);
 }
 
-template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, bool GREC = false>
+template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, int GREC = 0>
 hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
     static_assert(KIND != K_PAIR || (BLOCK == 128 && HIT_LDS && !BVH && !GREC), "pair launches: 128 lanes, 64 pixels");
     static_assert(KIND == K_SIMPLE || !BVH, "BVH scenes: the ray-refill kernel");
@@ -1685,7 +1506,7 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     std::snprintf(rt_launched_kernel, sizeof rt_launched_kernel, "%s<%d%s%s%s>%s",
                   KIND == K_PAIR ? "rt_render_pair_kernel" : KIND == K_SORTED ? "rt_render_sorted_kernel" : "rt_render_kernel",
-                  KIND == K_PAIR ? 128 : BLOCK, HIT_LDS ? "" : ",hit_global", GREC ? ",grec" : "", BVH ? ",bvh" : "",
+                  KIND == K_PAIR ? 128 : BLOCK, HIT_LDS ? "" : ",hit_global", GREC == 2 ? ",grec8" : GREC ? ",grec" : "", BVH ? ",bvh" : "",
                   feedback ? "+order" : "");
     hipError_t e = hipGetLastError();
     // the sort runs when asked, and always for a grid without an order yet
@@ -1772,58 +1593,90 @@ hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_
         if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
             return rt_launch_render_bvh_simple(K, BLOCK, lds, grid_mult, num_cus, s);
     }
+    if (KIND == K_SORTED && K.rec && K.grec_mode == 2) {
+        // the 8-wave shape exists for 256-lane groups with the hit table in
+        // LDS; any other launch takes the 7-wave shape (its global levels fit
+        // the mode-2 buffer: fewer of them)
+        if constexpr (KIND == K_SORTED && BLOCK == 256) {
+            if (hit_lds) return launch_render<KIND, BLOCK, true, false, 2>(K, lds, grid_mult, num_cus, s);
+        }
+        rt_kparams K1 = K;
+        K1.grec_mode = 1;
+        return launch_block<BLOCK, KIND>(K1, hit_lds, rt_render_lds_bytes(K1, BLOCK, hit_lds, true), grid_mult, num_cus, s);
+    }
     if (KIND == K_SORTED && K.rec)  // record stack in global memory
-        return hit_lds ? launch_render<KIND, BLOCK, true, false, true>(K, lds, grid_mult, num_cus, s)
-                       : launch_render<KIND, BLOCK, false, false, true>(K, lds, grid_mult, num_cus, s);
+        return hit_lds ? launch_render<KIND, BLOCK, true, false, 1>(K, lds, grid_mult, num_cus, s)
+                       : launch_render<KIND, BLOCK, false, false, 1>(K, lds, grid_mult, num_cus, s);
     return hit_lds ? launch_render<KIND, BLOCK, true>(K, lds, grid_mult, num_cus, s)
                    : launch_render<KIND, BLOCK, false>(K, lds, grid_mult, num_cus, s);
 }
 }  // namespace
 
-// Launch policy for the sorted kernel's record stack: global memory when the
-// LDS stack (3 dwords per level per lane) would hold the brute-force kernel
-// below RT_WAVES_PER_EU waves per SIMD, i.e. deep paths.  Measured: config
-// 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms.
+// Launch policy for the sorted kernel's record stack (K.grec_mode): global
+// memory when the LDS stack (3 dwords per level per lane) would hold the
+// brute-force kernel below RT_WAVES_PER_EU waves per SIMD, i.e. deep paths.
+// Measured: config 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms.
 // Also when global records let more 256-lane groups reside per CU (runtime
-// occupancy of both instantiations) and the frame runs at least
+// occupancy of the instantiations) and the frame runs at least
 // RT_GREC_MIN_GEN generations of them: config 3 (maxBounces 4) 6 -> 7
 // waves/SIMD, 0.816 -> 0.801 ms (three alternating runs); re-measured in
 // round 5 on its row shards (`profiles/r05b/ab_grec_shards.txt`): 1/2 (2.26
 // generations) 0.460 -> 0.453 ms, 1/3 (1.51) 0.335 -> 0.322, but 1/4 (1.13)
-// 0.270 -> 0.277; config 2 gains no group
+// 0.270 -> 0.277; config 2 gains no group.  Mode 2 (one LDS level, 8 waves
+// per SIMD) when it, and neither other shape, holds the whole frame in one
+// resident generation (the c3 1/4 shard: 2,025 pixels per CU, 1.32
+// generations of LDS records, 0.99 of mode 2).
+// req: the BWRT_GREC knob (-1 = policy, 0 / 1 / 2 = that shape).
 #ifndef RT_GREC_MIN_GEN
 #define RT_GREC_MIN_GEN 1.4
 #endif
-bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
-    if (K.bvh_nodes || K.max_bounces <= 0) return false;
+#ifndef RT_GREC8_MAX_GEN
+#define RT_GREC8_MAX_GEN 1.0
+#endif
+int rt_render_global_records(const rt_kparams& K, int num_cus, int req) {
+    if (K.bvh_nodes || (req < 0 && K.max_bounces <= 0)) return 0;
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
+    if (req >= 0) return req == 2 && !hit_lds ? 1 : req > 2 ? 1 : req;
     rt_kparams L = K;
     L.rec = nullptr;
     const size_t lds = rt_render_lds_bytes(L, 256, hit_lds, true);
     const long groups = (long)(160 * 1024) / (long)(lds ? lds : 1);  // 256-lane groups per CU: 1 wave per SIMD each
-    if (groups < RT_WAVES_PER_EU) return true;
+    if (groups < RT_WAVES_PER_EU) return 1;
     // resident 256-lane groups per CU with LDS / global records
     L.rec = reinterpret_cast<float*>(&L);  // any non-null: the global-record LDS size
+    L.grec_mode = 1;
     const size_t lds_g = rt_render_lds_bytes(L, 256, hit_lds, true);
-    int occ_l = 0, occ_g = 0;
+    L.grec_mode = 2;
+    const size_t lds_8 = rt_render_lds_bytes(L, 256, hit_lds, true);
+    int occ_l = 0, occ_g = 0, occ_8 = 0;
     const void* kl = hit_lds ? kernel_ptr<K_SORTED, 256, true>() : kernel_ptr<K_SORTED, 256, false>();
-    const void* kg = hit_lds ? kernel_ptr<K_SORTED, 256, true, false, true>() : kernel_ptr<K_SORTED, 256, false, false, true>();
+    const void* kg = hit_lds ? kernel_ptr<K_SORTED, 256, true, false, 1>() : kernel_ptr<K_SORTED, 256, false, false, 1>();
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_l, kl, 256, lds) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_g, kg, 256, lds_g) != hipSuccess || occ_g <= occ_l)
-        return false;
-    const double gens = (double)((long)K.rows * K.width) / (256.0 * occ_g * (num_cus > 0 ? num_cus : 1));
-    return gens >= RT_GREC_MIN_GEN;
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_g, kg, 256, lds_g) != hipSuccess)
+        return 0;
+    if (hit_lds &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_8, kernel_ptr<K_SORTED, 256, true, false, 2>(), 256, lds_8) !=
+            hipSuccess)
+        occ_8 = 0;
+    const double per_gen = 256.0 * (num_cus > 0 ? num_cus : 1);
+    const double px = (double)((long)K.rows * K.width);
+    if (occ_8 > occ_g && occ_8 > occ_l && px <= RT_GREC8_MAX_GEN * per_gen * occ_8 &&
+        px > per_gen * (occ_g > occ_l ? occ_g : occ_l))
+        return 2;
+    if (occ_g <= occ_l) return 0;
+    return px / (per_gen * occ_g) >= RT_GREC_MIN_GEN ? 1 : 0;
 }
 
 // Floats of a global-memory record stack for one launch: 3 dwords per level
-// kept in global memory (levels RT_GREC_LDS_LEVELS .. max_bounces-1; the
+// kept in global memory (levels grec_lds_levels(mode) .. max_bounces-1; the
 // shallow ones stay in LDS) per lane of the grid (the grid covers every work
 // item, rounded up to the largest workgroup), [group][level][field][lane].  At least one float, so a
 // forced global-record launch with no global level still gets a buffer.
 size_t rt_render_rec_floats(const rt_kparams& K) {
     const long nitems = launch_items(K);
-    const int lds_levels = K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS;
+    const int ll = grec_lds_levels(K.grec_mode);
+    const int lds_levels = K.max_bounces < ll ? K.max_bounces : ll;
     const size_t planes = (size_t)3 * (K.max_bounces - lds_levels);
     return planes ? planes * (size_t)((nitems + 255) / 256 * 256) : 1;
 }
@@ -1834,8 +1687,8 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
-    const int lds_levels = sorted && K.rec ? (K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS)
-                                           : K.max_bounces + (sorted ? 0 : 1);
+    const int ll = grec_lds_levels(K.grec_mode);
+    const int lds_levels = sorted && K.rec ? (K.max_bounces < ll ? K.max_bounces : ll) : K.max_bounces + (sorted ? 0 : 1);
     size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * block * sizeof(float);
     if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);  // + queue counters
     return b;

@@ -47,6 +47,10 @@
 #define RT_PI 3.1415926535f        // Math.cuh:5
 #define RT_MAX_LEVELS 33           // recursion records per path: RT_MAX_BOUNCES (rt_abi.h) + 1
 
+// diagnostic builds (-DRT_GTIMES, BWRT_GTIMES): words of the group / lane
+// time buffer (rt_diag.h; rt_context.cpp allocates it)
+#define RT_GTIMES_WORDS (1ull << 22)
+
 struct rt_kparams {
     int width, height;          // full image
     int row_offset, row_stride; // shard rows y = row_offset + j*row_stride
@@ -112,6 +116,7 @@ struct rt_kparams {
     // grid, [group][level - RT_GREC_LDS_LEVELS][field][lane]; null = all
     // records in LDS
     float* rec;
+    int grec_mode;              // shape of a global-record launch (rt_kernels.hip grec_lds_levels): 1 or 2
     int rec_stride;             // lanes in the grid (set by the launcher)
     // launch-order feedback (sorted kernel): workgroup g renders tile-group
     // group_order[g] (null = g itself; a permutation of the grid's groups,

@@ -23,9 +23,34 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 os.environ.setdefault("BWRT_TUNING", "1")
 # a stray knob in the caller's environment would change which kernel every
 # default-policy test checks: only the tests themselves set them (BWRT_LIB
-# picks the library, BWRT_TUNING opens the gate)
-for _k in [k for k in os.environ if k.startswith("BWRT_") and k not in ("BWRT_LIB", "BWRT_TUNING")]:
-    del os.environ[_k]
+# picks the library, BWRT_TUNING opens the gate).  The one deliberate way in
+# is BWRT_AB_ENV="BWRT_X=1,BWRT_Y=2": tools/ab.sh's parity gate names a
+# candidate's launch knobs there, and they are re-applied after the strip
+# (and after every test), so the gate checks the candidate it reports on.
+_KEEP = ("BWRT_LIB", "BWRT_TUNING", "BWRT_AB_ENV")
+
+
+def ab_knobs(spec):
+    """Parse BWRT_AB_ENV: comma-separated BWRT_*=value pairs."""
+    out = {}
+    for item in filter(None, (spec or "").split(",")):
+        k, sep, v = item.partition("=")
+        if not sep or not k.startswith("BWRT_") or k in _KEEP:
+            raise ValueError(f"BWRT_AB_ENV: bad knob {item!r}")
+        out[k] = v
+    return out
+
+
+_AB_KNOBS = ab_knobs(os.environ.get("BWRT_AB_ENV"))
+
+
+def _reset_knobs():
+    for k in [k for k in os.environ if k.startswith("BWRT_") and k not in _KEEP]:
+        del os.environ[k]
+    os.environ.update(_AB_KNOBS)
+
+
+_reset_knobs()
 
 
 def pytest_configure(config):
@@ -38,8 +63,7 @@ def _no_stray_knobs():
     """Knobs a test sets through monkeypatch are undone by it; this catches
     any left behind by a test that set os.environ directly."""
     yield
-    for k in [k for k in os.environ if k.startswith("BWRT_") and k not in ("BWRT_LIB", "BWRT_TUNING")]:
-        del os.environ[k]
+    _reset_knobs()
 
 
 @pytest.fixture(scope="session")

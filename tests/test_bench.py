@@ -19,7 +19,12 @@ def bench():
     return mod
 
 
-def test_self_launch_command(bench):
+def test_self_launch_command(bench, monkeypatch):
+    # a stale rank identity in the caller's environment must not reach the
+    # children; an IPC mode the caller chose is kept
+    for k, v in (("RANK", "5"), ("LOCAL_RANK", "5"), ("WORLD_SIZE", "7"), ("MASTER_PORT", "1")):
+        monkeypatch.setenv(k, v)
+    monkeypatch.delenv("HSA_ENABLE_IPC_MODE_LEGACY", raising=False)
     argv = ["--gpus", "8", "--steps", "20", "--warmup", "5"]
     cmd, env = bench.self_launch_command(argv, 8, 29123)
     assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
@@ -28,7 +33,28 @@ def test_self_launch_command(bench):
     script = cmd.index(os.path.join(REPO, "bench.py"))
     assert cmd[script + 1:] == argv  # the same arguments reach every rank
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
-    assert "WORLD_SIZE" not in env or env["WORLD_SIZE"] == os.environ.get("WORLD_SIZE")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT"):
+        assert k not in env, k
+    monkeypatch.setenv("HSA_ENABLE_IPC_MODE_LEGACY", "1")
+    assert bench.self_launch_command(argv, 8, 29123)[1]["HSA_ENABLE_IPC_MODE_LEGACY"] == "1"
+
+
+def test_dist_flag_self_launches_one_rank(bench, monkeypatch):
+    """`--gpus 1 --dist` without a launcher starts one torch.distributed.run
+    rank (the multi-rank path at N = 1: RCCL group, gather, de-interleave)."""
+    calls = []
+
+    class Done:
+        returncode = 0
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "run", lambda cmd, env=None, **kw: calls.append(cmd) or Done())
+    monkeypatch.setattr(bench.torch.cuda, "set_device", lambda *a: pytest.fail("launcher touched the GPU"))
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "1", "--dist", "--steps", "3"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and len(calls) == 1
+    assert "--nproc-per-node=1" in calls[0] and calls[0][-5:] == ["--gpus", "1", "--dist", "--steps", "3"]
 
 
 @pytest.mark.parametrize("rc", [0, 3])

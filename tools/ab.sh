@@ -18,7 +18,9 @@ if [ -n "$SUBSET" ]; then
   for spec in "$@"; do
     IFS=: read -r label var envs <<< "$spec"
     K=(); [ "$SUBSET" = all ] || K=(-k "$SUBSET")
-    env BWRT_LIB=$(lib_of $var) ${envs//,/ } timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 120 \
+    # the knobs go through BWRT_AB_ENV: tests/conftest.py strips every other
+    # BWRT_* variable before the tests run
+    env BWRT_LIB=$(lib_of $var) BWRT_AB_ENV="$envs" timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 120 \
         --timeout-method thread "${K[@]}" > $OUT/pt_$label.log 2>&1 || { echo "$label parity FAILED"; tail -5 $OUT/pt_$label.log; exit 1; }
     echo "$label parity: $(tail -1 $OUT/pt_$label.log)"
   done
