@@ -71,7 +71,9 @@ def parse():
                     help="take the multi-rank path even at N = 1: process group (RCCL unless BWRT_DIST_BACKEND), "
                          "rooted gather of the row blocks, de-interleave kernel, verify against a solo render")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC record of this workload (default: profiles/traffic_<config>.json, then "
+                         "profiles/traffic_latest.json; used only when its workload key matches)")
     return ap.parse_args()
 
 
@@ -132,15 +134,35 @@ def cpu_baseline(lib, config, scene_key, w, h, spp, mb, threads, gpu_renderer=No
     return out
 
 
-def load_traffic(path, workload_key):
-    try:
-        with open(path) as f:
-            t = json.load(f)
+def load_traffic(paths, workload_key):
+    """The first PMC record (tools/make_traffic_json.py) among `paths` whose
+    workload key is this run's."""
+    for path in paths:
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
         if t.get("workload") == workload_key:
             return t
-    except (OSError, ValueError):
-        pass
     return None
+
+
+def traffic_paths(explicit, config):
+    if explicit:
+        return [explicit]
+    return [os.path.join(REPO, "profiles", f"traffic_{config}.json"),
+            os.path.join(REPO, "profiles", "traffic_latest.json")]
+
+
+# L1 (vector cache) line throughput per CU, tools/micro/ta_gather.hip:
+# dependent per-lane 16-byte gathers, 64 distinct 128-byte lines per
+# wave-load, cycles per wave-load per CU at 2.4 GHz / 64 — L1-resident lines
+# (16 KB footprint: hits, 64.14 cycles) and L2-served lines (4 MB footprint:
+# every line an L1 miss, 146.81 cycles) (profiles/r06a/ta_gather_micro.txt)
+L1_HIT_CYCLES_PER_LINE = 64.14 / 64
+L1_MISS_CYCLES_PER_LINE = 146.81 / 64
+L1_MICRO = "profiles/r06a/ta_gather_micro.txt"
 
 
 RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
@@ -347,7 +369,7 @@ def main():
         alg_bytes = units * BYTES_PER_PIXEL_PASS
         achieved = alg_bytes / (kern_avg_ms * 1e-3) / 1e9
         workload_key = f"{scene_key}-{W}x{H}-{SPP}spp-{MB}b-rows{world}"
-        traffic = load_traffic(args.traffic_json, workload_key)
+        traffic = load_traffic(traffic_paths(args.traffic_json, args.config), workload_key)
         out = {
             "metric": f"Msamples/sec (W*H*spp*bounces/t), {W}x{H} {SPP}spp {MB}-bounce, {SCENE_NAMES[scene_key]}",
             "value": round(value, 2),
@@ -399,6 +421,25 @@ def main():
                 "issue_frac": round(v["insts_valu_per_launch"] / ks / inst_peak, 4),
                 "active_lanes_per_valu": round(v["active_lanes_per_valu"], 2),
                 "counters": traffic.get("source")}
+        if traffic and traffic.get("l1"):
+            # the BVH walk's bound: the L1's line throughput.
+            # achieved = the launch's L1 tag accesses (one per distinct line
+            # per wave-load) / the kernel's time; peak = 256 CUs x the
+            # micro-benchmark's L1-hit rate (1 line per cycle) x 2.4 GHz.
+            # model_floor_ms: the launch's hits and misses (L1->L2 requests)
+            # each at the micro-benchmark's cycles per line
+            l1 = traffic["l1"]
+            tags, miss = l1["tag_accesses_per_launch"], l1["l2_requests_per_launch"]
+            peak = 256 * 2.4e9 / L1_HIT_CYCLES_PER_LINE
+            achieved = tags / (kern_avg_ms * 1e-3)
+            floor_ms = ((tags - miss) * L1_HIT_CYCLES_PER_LINE + miss * L1_MISS_CYCLES_PER_LINE) / (256 * 2.4e9) * 1e3
+            out["l1_line_roofline"] = {
+                "bound": "l1_lines", "unit": "lines/s", "achieved": round(achieved), "peak": round(peak),
+                "frac": round(achieved / peak, 4), "tag_accesses_per_launch": round(tags),
+                "l2_requests_per_launch": round(miss), "cycles_per_hit_line": round(L1_HIT_CYCLES_PER_LINE, 3),
+                "cycles_per_miss_line": round(L1_MISS_CYCLES_PER_LINE, 3), "model_floor_ms": round(floor_ms, 3),
+                "model_floor_frac": round(floor_ms / kern_avg_ms, 4), "counters": traffic.get("source"),
+                "micro": L1_MICRO}
         if not distributed and not args.no_cpu_baseline:
             torch.cuda.synchronize(dev)
             with Renderer(dev_index, lib=lib) as check:

@@ -29,7 +29,7 @@
 #include "rt_layout.h"
 
 size_t rt_render_rec_floats(const rt_kparams& K);
-int rt_render_global_records(const rt_kparams& K, int num_cus, int req);
+bool rt_render_wants_global_records(const rt_kparams& K, int num_cus);
 hipError_t rt_launch_render(const rt_kparams& K, int num_cus, int grid_mult, bool simple, int block_req,
                             hipStream_t stream, int pair_req);
 hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride,
@@ -147,7 +147,7 @@ struct rt_context {
     bool order_stale = true;
     unsigned long long launches = 0;
     bool order_feedback = true;  // BWRT_ORDER=0: blockIdx order
-    int grec = -1;  // BWRT_GREC: 1 / 2 / 0 force global records (7-wave / 8-wave shape) / LDS records; -1 = policy
+    int grec = -1;  // BWRT_GREC: 1 / 0 force global / LDS records; -1 = launch policy
     void* host_rgba = nullptr;  // pinned staging for rt_render_multi
     size_t host_rgba_bytes = 0;
     int block = 0;               // BWRT_BLOCK: sorted-kernel workgroup lanes (0 = launch policy)
@@ -905,7 +905,7 @@ int rt_create(int device, rt_context** out) {
         if (t >= 0 && t <= 64 && (t & (t - 1)) == 0) c->tile_w = t;
     }
     if (const char* g = tuning_env("BWRT_TILE_SQ")) c->tile_sq = std::atoi(g) != 0;
-    if (const char* g = tuning_env("BWRT_GREC")) c->grec = std::atoi(g) == 2 ? 2 : std::atoi(g) ? 1 : 0;
+    if (const char* g = tuning_env("BWRT_GREC")) c->grec = std::atoi(g) ? 1 : 0;
     if (const char* g = tuning_env("BWRT_LEAF_BATCH")) c->leaf_batch = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = tuning_env("BWRT_REFILL")) c->refill = std::min(std::max(std::atoi(g), 1), 64);
     if (const char* g = tuning_env("BWRT_SPREAD")) c->spread = std::atoi(g) ? 1 : 0;
@@ -1598,8 +1598,7 @@ static int launch(rt_context* c, rt_kparams& K, hipStream_t s, unsigned first, i
     K.refill = c->refill > 0 ? c->refill : small ? RT_REFILL_SMALL : RT_REFILL;
     // deep paths: the sorted kernel's record stack in global memory (launch policy)
     K.rec = nullptr;
-    K.grec_mode = c->simple ? 0 : rt_render_global_records(K, c->num_cus, c->grec);
-    if (K.grec_mode) {
+    if (!c->simple && (c->grec == 1 || (c->grec < 0 && rt_render_wants_global_records(K, c->num_cus)))) {
         const int rc = ensure_buf(c, c->rec, rt_render_rec_floats(K) * sizeof(float));
         if (rc) return rc;
         K.rec = (float*)c->rec.p;

@@ -246,15 +246,6 @@ __device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
 #ifndef RT_GREC_LDS_LEVELS
 #define RT_GREC_LDS_LEVELS 2
 #endif
-// global-record shapes (template GREC of the sorted kernel, K.grec_mode):
-// 0 = the record stack in LDS; 1 = RT_GREC_LDS_LEVELS shallow levels in LDS
-// at RT_GREC_WAVES waves per SIMD (full frames, deep paths); 2 = one LDS
-// level at 8 waves per SIMD (64 VGPRs): 8 groups of 256 lanes per CU, for
-// frames and shards that fit one resident generation of it
-__host__ __device__ constexpr int grec_lds_levels(int mode) { return mode == 2 ? 1 : RT_GREC_LDS_LEVELS; }
-__host__ __device__ constexpr int sorted_waves_per_eu(int mode) {
-    return mode == 2 ? 8 : mode ? RT_GREC_WAVES : RT_WAVES_PER_EU;
-}
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
 #endif
@@ -511,8 +502,8 @@ enum { T_NONE = 0, T_REGEN = 1, T_DIFF = 2, T_SPEC = 3 };  // a lane's next task
 //      [task slots 13 x BLOCK, field-major][2 x 2 queue counters]
 // GREC: the record levels >= RT_GREC_LDS_LEVELS in global memory (deep paths
 // and full frames, launch policy).  BVH scenes take the ray-refill kernel.
-template <int BLOCK, bool HIT_LDS, int GREC, bool ORDER = false, bool QUADS = true>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(sorted_waves_per_eu(GREC))))
+template <int BLOCK, bool HIT_LDS, bool GREC, bool ORDER = false, bool QUADS = true>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GREC ? RT_GREC_WAVES : RT_WAVES_PER_EU)))
 rt_render_sorted_kernel(rt_kparams K) {
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
@@ -535,7 +526,7 @@ rt_render_sorted_kernel(rt_kparams K) {
     // reached) in global memory, [group][level - LL][field][lane] (each
     // group's records contiguous and coalesced), so LDS leaves room for
     // RT_GREC_WAVES waves and few records ever leave the CU
-    const int LL = GREC ? (levels < grec_lds_levels(GREC) ? levels : grec_lds_levels(GREC)) : levels;
+    const int LL = GREC ? (levels < RT_GREC_LDS_LEVELS ? levels : RT_GREC_LDS_LEVELS) : levels;
     // (an LDS-address-space pointer: 32-bit address arithmetic, no 64-bit
     // base held across the loop)
     lds_float* rec = (lds_float*)(rec_base + tid);
@@ -1429,7 +1420,7 @@ namespace {
 // and shards: 128 lanes for 64 pixels)
 enum { K_SIMPLE = 0, K_SORTED = 1, K_PAIR = 2 };
 
-template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, int GREC = 0, bool ORDER = false, bool QUADS = true>
+template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, bool GREC = false, bool ORDER = false, bool QUADS = true>
 void* kernel_ptr() {
     if constexpr (KIND == K_PAIR) return reinterpret_cast<void*>(&rt_render_pair_kernel<HIT_LDS, ORDER, QUADS>);
     if constexpr (KIND == K_SORTED)
@@ -1437,7 +1428,7 @@ void* kernel_ptr() {
     return reinterpret_cast<void*>(&rt_render_kernel<BLOCK, HIT_LDS, BVH>);
 }
 
-template <int KIND, int BLOCK, bool HIT_LDS, int GREC, bool ORDER, bool QUADS>
+template <int KIND, int BLOCK, bool HIT_LDS, bool GREC, bool ORDER, bool QUADS>
 void launch_kind(const rt_kparams& K, long grid, size_t lds, hipStream_t stream) {
     if constexpr (KIND == K_PAIR)
         hipLaunchKernelGGL((rt_render_pair_kernel<HIT_LDS, ORDER, QUADS>), dim3((unsigned)grid), dim3(128), lds, stream, K);
@@ -1446,7 +1437,7 @@ void launch_kind(const rt_kparams& K, long grid, size_t lds, hipStream_t stream)
                            dim3(BLOCK), lds, stream, K);
 }
 
-template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, int GREC = 0>
+template <int KIND, int BLOCK, bool HIT_LDS, bool BVH = false, bool GREC = false>
 hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int num_cus, hipStream_t stream) {
     static_assert(KIND != K_PAIR || (BLOCK == 128 && HIT_LDS && !BVH && !GREC), "pair launches: 128 lanes, 64 pixels");
     static_assert(KIND == K_SIMPLE || !BVH, "BVH scenes: the ray-refill kernel");
@@ -1506,7 +1497,7 @@ hipError_t launch_render(const rt_kparams& K0, size_t lds, int grid_mult, int nu
     }
     std::snprintf(rt_launched_kernel, sizeof rt_launched_kernel, "%s<%d%s%s%s>%s",
                   KIND == K_PAIR ? "rt_render_pair_kernel" : KIND == K_SORTED ? "rt_render_sorted_kernel" : "rt_render_kernel",
-                  KIND == K_PAIR ? 128 : BLOCK, HIT_LDS ? "" : ",hit_global", GREC == 2 ? ",grec8" : GREC ? ",grec" : "", BVH ? ",bvh" : "",
+                  KIND == K_PAIR ? 128 : BLOCK, HIT_LDS ? "" : ",hit_global", GREC ? ",grec" : "", BVH ? ",bvh" : "",
                   feedback ? "+order" : "");
     hipError_t e = hipGetLastError();
     // the sort runs when asked, and always for a grid without an order yet
@@ -1593,90 +1584,62 @@ hipError_t launch_block(const rt_kparams& K, bool hit_lds, size_t lds, int grid_
         if (K.bvh_nodes)  // large scenes: hit table in global memory, BVH traversal
             return rt_launch_render_bvh_simple(K, BLOCK, lds, grid_mult, num_cus, s);
     }
-    if (KIND == K_SORTED && K.rec && K.grec_mode == 2) {
-        // the 8-wave shape exists for 256-lane groups with the hit table in
-        // LDS; any other launch takes the 7-wave shape (its global levels fit
-        // the mode-2 buffer: fewer of them)
-        if constexpr (KIND == K_SORTED && BLOCK == 256) {
-            if (hit_lds) return launch_render<KIND, BLOCK, true, false, 2>(K, lds, grid_mult, num_cus, s);
-        }
-        rt_kparams K1 = K;
-        K1.grec_mode = 1;
-        return launch_block<BLOCK, KIND>(K1, hit_lds, rt_render_lds_bytes(K1, BLOCK, hit_lds, true), grid_mult, num_cus, s);
-    }
     if (KIND == K_SORTED && K.rec)  // record stack in global memory
-        return hit_lds ? launch_render<KIND, BLOCK, true, false, 1>(K, lds, grid_mult, num_cus, s)
-                       : launch_render<KIND, BLOCK, false, false, 1>(K, lds, grid_mult, num_cus, s);
+        return hit_lds ? launch_render<KIND, BLOCK, true, false, true>(K, lds, grid_mult, num_cus, s)
+                       : launch_render<KIND, BLOCK, false, false, true>(K, lds, grid_mult, num_cus, s);
     return hit_lds ? launch_render<KIND, BLOCK, true>(K, lds, grid_mult, num_cus, s)
                    : launch_render<KIND, BLOCK, false>(K, lds, grid_mult, num_cus, s);
 }
 }  // namespace
 
-// Launch policy for the sorted kernel's record stack (K.grec_mode): global
-// memory when the LDS stack (3 dwords per level per lane) would hold the
-// brute-force kernel below RT_WAVES_PER_EU waves per SIMD, i.e. deep paths.
-// Measured: config 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms.
+// Launch policy for the sorted kernel's record stack: global memory when the
+// LDS stack (3 dwords per level per lane) would hold the brute-force kernel
+// below RT_WAVES_PER_EU waves per SIMD, i.e. deep paths.  Measured: config
+// 4 (maxBounces 6) 4 -> 7 waves/SIMD, 7.61 -> 6.34 ms.
 // Also when global records let more 256-lane groups reside per CU (runtime
-// occupancy of the instantiations) and the frame runs at least
+// occupancy of both instantiations) and the frame runs at least
 // RT_GREC_MIN_GEN generations of them: config 3 (maxBounces 4) 6 -> 7
 // waves/SIMD, 0.816 -> 0.801 ms (three alternating runs); re-measured in
 // round 5 on its row shards (`profiles/r05b/ab_grec_shards.txt`): 1/2 (2.26
 // generations) 0.460 -> 0.453 ms, 1/3 (1.51) 0.335 -> 0.322, but 1/4 (1.13)
-// 0.270 -> 0.277; config 2 gains no group.  Mode 2 (one LDS level, 8 waves
-// per SIMD) when it, and neither other shape, holds the whole frame in one
-// resident generation (the c3 1/4 shard: 2,025 pixels per CU, 1.32
-// generations of LDS records, 0.99 of mode 2).
-// req: the BWRT_GREC knob (-1 = policy, 0 / 1 / 2 = that shape).
+// 0.270 -> 0.277; config 2 gains no group.  A third shape, one LDS level at
+// 8 waves per SIMD (64 VGPRs, 8-byte spill), makes the 1/4 shard one resident
+// generation (0.99) instead of 1.32, and loses there: 0.298 vs 0.270 ms with
+// LDS records, 1/2 0.455 vs 0.42, full frame flat (round 6, two alternating
+// runs, profiles/r06a/ab_grec.txt; the code: profiles/r06a/grec8_shape.diff)
 #ifndef RT_GREC_MIN_GEN
 #define RT_GREC_MIN_GEN 1.4
 #endif
-#ifndef RT_GREC8_MAX_GEN
-#define RT_GREC8_MAX_GEN 1.0
-#endif
-int rt_render_global_records(const rt_kparams& K, int num_cus, int req) {
-    if (K.bvh_nodes || (req < 0 && K.max_bounces <= 0)) return 0;
+bool rt_render_wants_global_records(const rt_kparams& K, int num_cus) {
+    if (K.bvh_nodes || K.max_bounces <= 0) return false;
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const bool hit_lds = (size_t)n_prim * RT_HIT_FLOATS * sizeof(float) <= 16384;
-    if (req >= 0) return req == 2 && !hit_lds ? 1 : req > 2 ? 1 : req;
     rt_kparams L = K;
     L.rec = nullptr;
     const size_t lds = rt_render_lds_bytes(L, 256, hit_lds, true);
     const long groups = (long)(160 * 1024) / (long)(lds ? lds : 1);  // 256-lane groups per CU: 1 wave per SIMD each
-    if (groups < RT_WAVES_PER_EU) return 1;
+    if (groups < RT_WAVES_PER_EU) return true;
     // resident 256-lane groups per CU with LDS / global records
     L.rec = reinterpret_cast<float*>(&L);  // any non-null: the global-record LDS size
-    L.grec_mode = 1;
     const size_t lds_g = rt_render_lds_bytes(L, 256, hit_lds, true);
-    L.grec_mode = 2;
-    const size_t lds_8 = rt_render_lds_bytes(L, 256, hit_lds, true);
-    int occ_l = 0, occ_g = 0, occ_8 = 0;
+    int occ_l = 0, occ_g = 0;
     const void* kl = hit_lds ? kernel_ptr<K_SORTED, 256, true>() : kernel_ptr<K_SORTED, 256, false>();
-    const void* kg = hit_lds ? kernel_ptr<K_SORTED, 256, true, false, 1>() : kernel_ptr<K_SORTED, 256, false, false, 1>();
+    const void* kg = hit_lds ? kernel_ptr<K_SORTED, 256, true, false, true>() : kernel_ptr<K_SORTED, 256, false, false, true>();
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_l, kl, 256, lds) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_g, kg, 256, lds_g) != hipSuccess)
-        return 0;
-    if (hit_lds &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_8, kernel_ptr<K_SORTED, 256, true, false, 2>(), 256, lds_8) !=
-            hipSuccess)
-        occ_8 = 0;
-    const double per_gen = 256.0 * (num_cus > 0 ? num_cus : 1);
-    const double px = (double)((long)K.rows * K.width);
-    if (occ_8 > occ_g && occ_8 > occ_l && px <= RT_GREC8_MAX_GEN * per_gen * occ_8 &&
-        px > per_gen * (occ_g > occ_l ? occ_g : occ_l))
-        return 2;
-    if (occ_g <= occ_l) return 0;
-    return px / (per_gen * occ_g) >= RT_GREC_MIN_GEN ? 1 : 0;
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_g, kg, 256, lds_g) != hipSuccess || occ_g <= occ_l)
+        return false;
+    const double gens = (double)((long)K.rows * K.width) / (256.0 * occ_g * (num_cus > 0 ? num_cus : 1));
+    return gens >= RT_GREC_MIN_GEN;
 }
 
 // Floats of a global-memory record stack for one launch: 3 dwords per level
-// kept in global memory (levels grec_lds_levels(mode) .. max_bounces-1; the
+// kept in global memory (levels RT_GREC_LDS_LEVELS .. max_bounces-1; the
 // shallow ones stay in LDS) per lane of the grid (the grid covers every work
 // item, rounded up to the largest workgroup), [group][level][field][lane].  At least one float, so a
 // forced global-record launch with no global level still gets a buffer.
 size_t rt_render_rec_floats(const rt_kparams& K) {
     const long nitems = launch_items(K);
-    const int ll = grec_lds_levels(K.grec_mode);
-    const int lds_levels = K.max_bounces < ll ? K.max_bounces : ll;
+    const int lds_levels = K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS;
     const size_t planes = (size_t)3 * (K.max_bounces - lds_levels);
     return planes ? planes * (size_t)((nitems + 255) / 256 * 256) : 1;
 }
@@ -1687,8 +1650,8 @@ size_t rt_render_lds_bytes(const rt_kparams& K, int block, bool hit_lds, bool so
     const int n_prim = K.n_sph + K.n_pln + K.n_tri + K.n_quad;
     const size_t hit = hit_lds ? (size_t)((n_prim * RT_HIT_FLOATS + 3) & ~3) * sizeof(float) : 0;
     // record stack: max_bounces + 1 levels (simple kernel), max_bounces (sorted)
-    const int ll = grec_lds_levels(K.grec_mode);
-    const int lds_levels = sorted && K.rec ? (K.max_bounces < ll ? K.max_bounces : ll) : K.max_bounces + (sorted ? 0 : 1);
+    const int lds_levels = sorted && K.rec ? (K.max_bounces < RT_GREC_LDS_LEVELS ? K.max_bounces : RT_GREC_LDS_LEVELS)
+                                           : K.max_bounces + (sorted ? 0 : 1);
     size_t b = hit + (size_t)3 * (lds_levels > 0 ? lds_levels : 0) * block * sizeof(float);
     if (sorted) b += (size_t)13 * block * sizeof(float) + 8 * sizeof(int);  // + queue counters
     return b;

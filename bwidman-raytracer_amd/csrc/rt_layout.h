@@ -116,7 +116,6 @@ struct rt_kparams {
     // grid, [group][level - RT_GREC_LDS_LEVELS][field][lane]; null = all
     // records in LDS
     float* rec;
-    int grec_mode;              // shape of a global-record launch (rt_kernels.hip grec_lds_levels): 1 or 2
     int rec_stride;             // lanes in the grid (set by the launcher)
     // launch-order feedback (sorted kernel): workgroup g renders tile-group
     // group_order[g] (null = g itself; a permutation of the grid's groups,

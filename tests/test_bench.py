@@ -93,3 +93,22 @@ def test_rank_under_torchrun_does_not_relaunch(bench, monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert "WORLD_SIZE=4" in str(e.value.code)
+
+
+def test_traffic_record_is_per_workload(bench, tmp_path):
+    """The PMC record (tools/make_traffic_json.py) is looked up per config
+    (profiles/traffic_<config>.json, then traffic_latest.json) and used only
+    when its workload key is this run's."""
+    import json
+    a, b = tmp_path / "traffic_c5.json", tmp_path / "traffic_latest.json"
+    a.write_text(json.dumps({"workload": "stress-1920x1080-32spp-8b-rows1", "l1": {"tag_accesses_per_launch": 1}}))
+    b.write_text(json.dumps({"workload": "07-1920x1080-8spp-4b-rows1"}))
+    assert bench.load_traffic([str(a), str(b)], "stress-1920x1080-32spp-8b-rows1")["l1"]
+    assert bench.load_traffic([str(a), str(b)], "07-1920x1080-8spp-4b-rows1") == {"workload": "07-1920x1080-8spp-4b-rows1"}
+    assert bench.load_traffic([str(a), str(b)], "07-1920x1080-8spp-4b-rows2") is None
+    assert bench.load_traffic([str(tmp_path / "missing.json")], "x") is None
+    paths = bench.traffic_paths(None, "c5")
+    assert paths[0].endswith("profiles/traffic_c5.json") and paths[1].endswith("profiles/traffic_latest.json")
+    assert bench.traffic_paths("/x.json", "c5") == ["/x.json"]
+    # the L1 line peak: 256 CUs at the micro-benchmark's one L1-hit line per cycle
+    assert 0.95 < bench.L1_HIT_CYCLES_PER_LINE < 1.05 and bench.L1_MISS_CYCLES_PER_LINE > 2

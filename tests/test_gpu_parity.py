@@ -74,11 +74,10 @@ def test_config3_07_full_size(gpu, oracle):
 # (rank r of G renders rows y = r mod G), plus 6 rows apart, the pair kernel's
 # boundary (345,600 pixels <= 256 CUs x RT_SPREAD_PIX 1,400), each through the
 # DEFAULT launch policy and the kernel it picks for that shard (global
-# records from RT_GREC_MIN_GEN = 1.4 resident generations: 1/2 has 2.26; the
-# 8-wave shape where it alone makes the shard one resident generation: 1/4,
-# 0.99 of it)
+# records from RT_GREC_MIN_GEN = 1.4 resident generations: 1/2 has 2.26, 1/4
+# 1.13)
 @pytest.mark.parametrize("stride,offset,kernel", [(2, 1, "rt_render_sorted_kernel<256,grec>"),
-                                                  (4, 3, "rt_render_sorted_kernel<256,grec8>"),
+                                                  (4, 3, "rt_render_sorted_kernel<256>"),
                                                   (6, 2, "rt_render_pair_kernel<128>"),
                                                   (8, 5, "rt_render_pair_kernel<128>")])
 def test_config3_shards(gpu, oracle, stride, offset, kernel):
@@ -819,23 +818,18 @@ def _fresh_renderer(bwrt_lib, monkeypatch, **env):
             monkeypatch.delenv(k)
 
 
-@pytest.mark.parametrize("grec,block", [(1, 64), (1, 128), (1, 256), (2, 256), (2, 128)])
+@pytest.mark.parametrize("block", [64, 128, 256])
 @pytest.mark.parametrize("w,h,mb", [(160, 90, 4), (100, 37, 6), (160, 90, 2), (120, 70, 3), (64, 40, 0)])
-def test_global_records_forced(bwrt_lib, oracle, monkeypatch, grec, block, w, h, mb):
+def test_global_records_forced(bwrt_lib, oracle, monkeypatch, block, w, h, mb):
     """The sorted kernel with its recursion records in global memory
     (BWRT_GREC=1; the launch policy picks it for deep paths such as config 4)
     at every workgroup size, including ragged sizes and a row shard.  Levels
     0-1 stay in LDS: at max_bounces 2 no level reaches global memory, at 3
-    exactly one does (the boundaries of the split).  BWRT_GREC=2: the 8-wave
-    shape (one LDS level: max_bounces 2 puts level 1 in global memory), which
-    exists for 256-lane groups; a 128-lane launch falls back to the 7-wave
-    shape inside the mode-2 buffer."""
-    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_GREC=grec, BWRT_BLOCK=block)
+    exactly one does (the boundaries of the split)."""
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_GREC=1, BWRT_BLOCK=block)
     try:
         for off, stride in ((0, 1), (1, 3)):
             img, st = run_pair(r, oracle, scenes.scene_07(), w, h, 3, mb, row_offset=off, row_stride=stride)
-            if mb > 0:
-                assert_kernel(r, f"rt_render_sorted_kernel<{block},{'grec8' if (grec, block) == (2, 256) else 'grec'}>")
             assert np.array_equal(img, st.rgba)
             same_state(r, st)
             # continuation (frames 4-5 in a second launch): the deferred fold

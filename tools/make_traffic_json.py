@@ -40,6 +40,14 @@ def main():
             "active_lanes_per_valu": avg.get("SQ_THREAD_CYCLES_VALU", 0) / avg["SQ_INSTS_VALU"],
             "waves": avg.get("SQ_WAVES"),
         }
+    if "TCP_TOTAL_CACHE_ACCESSES_sum" in avg:
+        # L1 (vector cache) line accesses: tag lookups and the lines it
+        # requests from L2 (its misses), per launch — bench.py's
+        # l1_line_roofline
+        rec["l1"] = {
+            "tag_accesses_per_launch": avg["TCP_TOTAL_CACHE_ACCESSES_sum"],
+            "l2_requests_per_launch": avg.get("TCP_TCC_READ_REQ_sum"),
+        }
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec, indent=1))

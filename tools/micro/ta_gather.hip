@@ -44,20 +44,24 @@ int main() {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     const int grid = 256 * 16, iters = 2000;
+    // footprint: 4 MB (L2-resident, every distinct line an L1 miss) and
+    // 16 KB (128 lines: L1-resident after the first touch, L1 hits)
+    for (size_t fp : {lines, (size_t)128})
     for (int w : {1, 2, 4})
         for (int share : {1, 2, 4, 8, 16, 64}) {
+            if (fp != lines && w != 4) continue;
             for (int rep = 0; rep < 2; rep++) {
                 hipEventRecord(e0);
-                if (w == 4) hipLaunchKernelGGL(gather<4>, dim3(grid), dim3(256), 0, 0, buf, (unsigned)(lines - 1), share, iters, out);
-                if (w == 2) hipLaunchKernelGGL(gather<2>, dim3(grid), dim3(256), 0, 0, buf, (unsigned)(lines - 1), share, iters, out);
-                if (w == 1) hipLaunchKernelGGL(gather<1>, dim3(grid), dim3(256), 0, 0, buf, (unsigned)(lines - 1), share, iters, out);
+                if (w == 4) hipLaunchKernelGGL(gather<4>, dim3(grid), dim3(256), 0, 0, buf, (unsigned)(fp - 1), share, iters, out);
+                if (w == 2) hipLaunchKernelGGL(gather<2>, dim3(grid), dim3(256), 0, 0, buf, (unsigned)(fp - 1), share, iters, out);
+                if (w == 1) hipLaunchKernelGGL(gather<1>, dim3(grid), dim3(256), 0, 0, buf, (unsigned)(fp - 1), share, iters, out);
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
                 float ms;
                 hipEventElapsedTime(&ms, e0, e1);
                 const double winst = (double)grid * 4 * iters;  // wave-level load instructions
-                if (rep) printf("dwords/lane %d  lanes per line %2d: %.3f ms  %.2f G wave-loads/s  %.2f cycles per wave-load per CU\n",
-                                w, share, ms, winst / ms / 1e6, ms * 1e-3 * 2.4e9 * 256 / winst);
+                if (rep) printf("footprint %7zu B  dwords/lane %d  lanes per line %2d: %.3f ms  %.2f G wave-loads/s  %.2f cycles per wave-load per CU\n",
+                                fp * 128, w, share, ms, winst / ms / 1e6, ms * 1e-3 * 2.4e9 * 256 / winst);
             }
         }
     return 0;
