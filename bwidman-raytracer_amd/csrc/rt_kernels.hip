@@ -249,14 +249,6 @@ __device__ __forceinline__ int prim_key(const rt_kparams& K, int id) {
 #ifndef RT_SPEC_PRIO
 #define RT_SPEC_PRIO 3
 #endif
-// s_setprio of the waves with at least RT_IPHASE_PRIO_MIN rays during the
-// I-phase's closest hit (A/B knob; 0 disables)
-#ifndef RT_IPHASE_PRIO
-#define RT_IPHASE_PRIO 0
-#endif
-#ifndef RT_IPHASE_PRIO_MIN
-#define RT_IPHASE_PRIO_MIN 48
-#endif
 // occupancy target of the pair kernel
 #ifndef RT_PAIR_WAVES
 #define RT_PAIR_WAVES 7
@@ -766,17 +758,10 @@ rt_render_sorted_kernel(rt_kparams K) {
         // ---- I-phase: closest hit + brdfChoice (Main.cu:214-245)
         float t = INFINITY;
         int id = -1;
-#if RT_IPHASE_PRIO
-        // the waves with the most rays run the longest closest hits: let them issue first
-        if (__popcll(__ballot(has_ray)) >= RT_IPHASE_PRIO_MIN) __builtin_amdgcn_s_setprio(RT_IPHASE_PRIO);
-#endif
         if (has_ray) {
             RT_TWICE_HIT(QUADS, K, o, d);
             closest_hit_brute<QUADS>(K, o, d, t, id);
         }
-#if RT_IPHASE_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
         if (has_ray) {
             has_ray = false;
             if (id >= 0) {
