@@ -37,7 +37,7 @@ hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offse
 extern thread_local long rt_order_groups_last;
 extern thread_local char rt_launched_kernel[96];
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
-                                  int shards, int rows_per_shard, hipStream_t stream);
+                                  int shards, int rows_per_shard, int max_blocks, hipStream_t stream);
 // scalar C++ CPU fallback (rt_cpu.cpp)
 int rt_cpu_render(const rt_kparams& K, int threads);
 void rt_cpu_init_rand(unsigned* rng, int width, int rows, int row_offset, int row_stride);
@@ -156,6 +156,7 @@ struct rt_context {
     int leaf_batch = -1;         // BWRT_LEAF_BATCH: BVH refill kernel leaf-batch threshold (-1 = launch policy)
     int refill = -1;             // BWRT_REFILL: BVH refill kernel refill threshold (-1 = launch policy)
     int spread = -1;             // BWRT_SPREAD: 1 / 0 force the pair kernel on / off (-1 = launch policy)
+    int deint_blocks = 0;        // BWRT_DEINT_BLOCKS: cap on the de-interleave grid (0 = one thread per 16 bytes)
     std::string kernel_name;     // the render kernel of the last launch (rt_last_kernel_name)
     unsigned frame = 1;
     int max_bounces = RT_DEFAULT_MAX_BOUNCES;
@@ -888,7 +889,16 @@ int rt_create(int device, rt_context** out) {
     if (device < 0 || device >= n) return RT_ERR_INVALID_ARGUMENT;
     rt_context* c = new rt_context();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    // BWRT_STREAM_PRIO=1: the context's stream at the device's highest
+    // priority (its workgroups dispatch ahead of other streams' — e.g. a
+    // multi-GPU gather and de-interleave overlapping the next render)
+    int prio_lo = 0, prio_hi = 0;
+    const char* sp = tuning_env("BWRT_STREAM_PRIO");
+    const bool high = sp && std::atoi(sp) == 1 && hipSetDevice(device) == hipSuccess &&
+                      hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) == hipSuccess;
+    if (hipSetDevice(device) != hipSuccess ||
+        (high ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi)
+              : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev_render) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_aux, hipEventDisableTiming) != hipSuccess) {
         rt_destroy(c);
@@ -898,6 +908,7 @@ int rt_create(int device, rt_context** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->num_cus = prop.multiProcessorCount;
     if (const char* gm = tuning_env("BWRT_GRID_MULT")) c->grid_mult = std::atoi(gm);
+    if (const char* db = tuning_env("BWRT_DEINT_BLOCKS")) c->deint_blocks = std::max(std::atoi(db), 0);
     if (const char* kk = tuning_env("BWRT_KERNEL")) c->simple = std::strcmp(kk, "simple") == 0;
     if (const char* bk = tuning_env("BWRT_BLOCK")) c->block = std::atoi(bk);
     if (const char* tw = tuning_env("BWRT_TILE")) {
@@ -1844,7 +1855,7 @@ int rt_deinterleave_rows_device(rt_context* c, const void* gathered, void* image
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     HIP_TRY(c, rt_launch_deinterleave((const unsigned*)gathered, (unsigned*)image, width, height, shards,
-                                      rows_per_shard, s));
+                                      rows_per_shard, c->deint_blocks, s));
     HIP_TRY(c, hipEventRecord(c->ev_aux, s));
     c->aux_recorded = true;
     return RT_OK;

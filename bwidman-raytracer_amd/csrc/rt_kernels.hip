@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <type_traits>
 
 #include "rt_diag.h"
 #include "rt_layout.h"
@@ -459,17 +460,23 @@ __global__ void __launch_bounds__(256) rt_init_rand_kernel(unsigned* rng, int wi
 }
 
 // Multi-GPU gather epilogue: block r of `gathered` holds rows r, r+G, ...
+// VEC = 4: 16 bytes (4 pixels) per lane (width % 4 == 0, 16-byte aligned
+// buffers); a grid-stride loop, so the launch may cap its grid and leave the
+// CUs to a render running beside it
+template <int VEC>
 __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const unsigned* __restrict__ gathered,
                                                               unsigned* __restrict__ image, int width,
                                                               int height, int shards, int rows_per_shard) {
-    const long n = (long)height * width;
-    const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    const int y = (int)(q / width);
-    const int x = (int)(q - (long)y * width);
-    const int r = y % shards;
-    const int j = y / shards;
-    image[q] = gathered[((long)r * rows_per_shard + j) * width + x];
+    typedef typename std::conditional<VEC == 4, uint4, unsigned>::type word;
+    const int wv = width / VEC;
+    const long n = (long)height * wv;
+    for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
+        const int y = (int)(q / wv);
+        const int x = (int)(q - (long)y * wv);
+        const int r = y % shards;
+        const int j = y / shards;
+        reinterpret_cast<word*>(image)[q] = reinterpret_cast<const word*>(gathered)[((long)r * rows_per_shard + j) * wv + x];
+    }
 }
 #endif  // RT_TU_BVH
 
@@ -1754,12 +1761,19 @@ hipError_t rt_launch_init_rand(unsigned* rng, int width, int rows, int row_offse
     return hipGetLastError();
 }
 
+// max_blocks > 0 caps the grid (the loop strides over the rest)
 hipError_t rt_launch_deinterleave(const unsigned* gathered, unsigned* image, int width, int height,
-                                  int shards, int rows_per_shard, hipStream_t stream) {
-    const long n = (long)height * width;
-    const unsigned grid = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(rt_deinterleave_kernel, dim3(grid), dim3(256), 0, stream, gathered, image,
-                       width, height, shards, rows_per_shard);
+                                  int shards, int rows_per_shard, int max_blocks, hipStream_t stream) {
+    const bool vec = width % 4 == 0 && ((reinterpret_cast<uintptr_t>(gathered) | reinterpret_cast<uintptr_t>(image)) & 15) == 0;
+    const long n = (long)height * (vec ? width / 4 : width);
+    long grid = (n + 255) / 256;
+    if (max_blocks > 0 && grid > max_blocks) grid = max_blocks;
+    if (vec)
+        hipLaunchKernelGGL(rt_deinterleave_kernel<4>, dim3((unsigned)grid), dim3(256), 0, stream, gathered, image,
+                           width, height, shards, rows_per_shard);
+    else
+        hipLaunchKernelGGL(rt_deinterleave_kernel<1>, dim3((unsigned)grid), dim3(256), 0, stream, gathered, image,
+                           width, height, shards, rows_per_shard);
     return hipGetLastError();
 }
 #endif  // RT_TU_BVH

@@ -112,3 +112,16 @@ def test_traffic_record_is_per_workload(bench, tmp_path):
     assert bench.traffic_paths("/x.json", "c5") == ["/x.json"]
     # the L1 line peak: 256 CUs at the micro-benchmark's one L1-hit line per cycle
     assert 0.95 < bench.L1_HIT_CYCLES_PER_LINE < 1.05 and bench.L1_MISS_CYCLES_PER_LINE > 2
+
+
+def test_oracle_check_leg(bench, bwrt_lib):
+    """The bench's oracle check (CPU-baseline leg, checker only) on config 1:
+    the renderer it is handed (here the product's CPU backend, on the GPU box
+    the GPU context) against the oracle, RGBA8 + frameSum + RNG; config 5 is
+    not checked there (the oracle's brute-force loop is minutes per row)."""
+    from bwrt import Renderer
+    with Renderer.cpu(2, lib=bwrt_lib) as r:
+        oc = bench.oracle_check("c1", "01", 256, 256, 1, 1, r)
+    assert oc["bit_exact"] is True and oc["rows"] == 256 and oc["row_stride"] == 1
+    assert bench.oracle_check("c5", "stress", 1920, 1080, 32, 8, None) is None
+    assert set(bench.ORACLE_ROW_STRIDE) == {"c1", "c2", "c3", "c4"}

@@ -520,20 +520,32 @@ def test_config4_shard_of_8(gpu, oracle):
     assert np.array_equal(img, st.rgba)
 
 
-def test_deinterleave_kernel(gpu):
+@pytest.mark.parametrize("blocks", [None, 3])
+def test_deinterleave_kernel(bwrt_lib, monkeypatch, blocks):
     """rt_deinterleave_rows_device (the multi-GPU gather epilogue) on device
-    buffers: gathered [shards][rows_per_shard][W] -> image [H][W]."""
+    buffers: gathered [shards][rows_per_shard][W] -> image [H][W] — 16 bytes
+    per lane when the width is a multiple of 4 and both buffers are 16-byte
+    aligned, 4 otherwise (odd widths, a buffer offset by one pixel); with
+    the grid capped at 3 blocks (BWRT_DEINT_BLOCKS) the loop strides over
+    the rest."""
     import torch
+    from bwrt import Renderer
     from bwrt.dist import ShardPlan, deinterleave_reference
-    for h, w, shards in [(1080, 1920, 8), (55, 33, 2), (7, 5, 3)]:
-        plan = ShardPlan(h, shards, 0)
-        g = torch.randint(0, 2**31 - 1, (shards * plan.rows_per_shard * w,), dtype=torch.int32, device="cuda")
-        out = torch.empty(h * w, dtype=torch.int32, device="cuda")
-        gpu.deinterleave_device(g.data_ptr(), out.data_ptr(), w, h, shards, plan.rows_per_shard,
-                                torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        want = deinterleave_reference(g.cpu().numpy().reshape(shards, plan.rows_per_shard, w, 1), plan, w)
-        assert np.array_equal(out.cpu().numpy().reshape(h, w), want[..., 0])
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_DEINT_BLOCKS=blocks) if blocks else Renderer(0, lib=bwrt_lib)
+    try:
+        for h, w, shards, off in [(1080, 1920, 8, 0), (2160, 3840, 8, 0), (1080, 1920, 1, 0), (36, 64, 4, 0),
+                                  (36, 64, 4, 1), (55, 33, 2, 0), (7, 5, 3, 0)]:
+            plan = ShardPlan(h, shards, 0)
+            g = torch.randint(0, 2**31 - 1, (shards * plan.rows_per_shard * w + off,), dtype=torch.int32,
+                              device="cuda")[off:]
+            out = torch.empty(h * w + off, dtype=torch.int32, device="cuda")[off:]
+            r.deinterleave_device(g.data_ptr(), out.data_ptr(), w, h, shards, plan.rows_per_shard,
+                                  torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            want = deinterleave_reference(g.cpu().numpy().reshape(shards, plan.rows_per_shard, w, 1), plan, w)
+            assert np.array_equal(out.cpu().numpy().reshape(h, w), want[..., 0]), (h, w, shards, off)
+    finally:
+        r.close()
 
 
 def test_render_device_into_torch_buffer(gpu, oracle):
