@@ -889,12 +889,15 @@ int rt_create(int device, rt_context** out) {
     if (device < 0 || device >= n) return RT_ERR_INVALID_ARGUMENT;
     rt_context* c = new rt_context();
     c->device = device;
-    // BWRT_STREAM_PRIO=1: the context's stream at the device's highest
-    // priority (its workgroups dispatch ahead of other streams' — e.g. a
-    // multi-GPU gather and de-interleave overlapping the next render)
+    // the context's stream at the device's highest priority: its render
+    // workgroups dispatch ahead of other streams' work, e.g. the multi-GPU
+    // gather and de-interleave of the previous frame that overlap the next
+    // render (world size 1, ms per step: 0.761-0.765 vs 0.780-0.785 at
+    // normal priority, single-GPU renders unchanged; profiles/r06e/);
+    // BWRT_STREAM_PRIO=0: normal priority
     int prio_lo = 0, prio_hi = 0;
     const char* sp = tuning_env("BWRT_STREAM_PRIO");
-    const bool high = sp && std::atoi(sp) == 1 && hipSetDevice(device) == hipSuccess &&
+    const bool high = !(sp && std::atoi(sp) == 0) && hipSetDevice(device) == hipSuccess &&
                       hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) == hipSuccess;
     if (hipSetDevice(device) != hipSuccess ||
         (high ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi)

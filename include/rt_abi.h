@@ -39,7 +39,9 @@
  *    result, only kernel choice and speed:
  *      at rt_create:    BWRT_KERNEL=simple, BWRT_BLOCK, BWRT_TILE, BWRT_TILE_SQ,
  *                       BWRT_GREC, BWRT_GRID_MULT, BWRT_LEAF_BATCH, BWRT_REFILL,
- *                       BWRT_SPREAD, BWRT_ORDER, BWRT_ORDER_PERIOD
+ *                       BWRT_SPREAD, BWRT_ORDER, BWRT_ORDER_PERIOD,
+ *                       BWRT_STREAM_PRIO=0 (the context's stream at normal
+ *                       instead of the highest priority), BWRT_DEINT_BLOCKS
  *      at rt_set_scene: BWRT_BVH_MIN, BWRT_BVH_LEAF, BWRT_BVH_CT, BWRT_BVH_SBVH,
  *                       BWRT_BVH_REFS, BWRT_BVH_ALPHA, BWRT_BVH_ORDER_MASK,
  *                       BWRT_BVH_N16, BWRT_NO_CULL, BWRT_BVH_STATS (report)
@@ -303,7 +305,9 @@ RT_API int rt_render_device(rt_context* ctx, const rt_render_params* p,
                             void* rgba_device, void* stream);
 
 /* The context's own HIP stream (hipStream_t), valid until rt_destroy (NULL
- * for a CPU context).  Renders on it (rt_render_device with this stream or
+ * for a CPU context), created at the device's highest stream priority, so a
+ * render on it dispatches ahead of work on the caller's other streams (a
+ * gather of the previous frame).  Renders on it (rt_render_device with this stream or
  * NULL) record their completion event lazily — when a later call needs it:
  * a render on another stream, a state read or write, rt_synchronize — so
  * back-to-back renders carry no marker packet between them (1.5-3 us per

@@ -539,6 +539,10 @@ def test_deinterleave_kernel(bwrt_lib, monkeypatch, blocks):
             g = torch.randint(0, 2**31 - 1, (shards * plan.rows_per_shard * w + off,), dtype=torch.int32,
                               device="cuda")[off:]
             out = torch.empty(h * w + off, dtype=torch.int32, device="cuda")[off:]
+            # (torch's default stream is the null stream, whose handle 0 means
+            # "the context's stream" to the C ABI: the inputs must be ready
+            # before a launch on another stream)
+            torch.cuda.synchronize()
             r.deinterleave_device(g.data_ptr(), out.data_ptr(), w, h, shards, plan.rows_per_shard,
                                   torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
