@@ -135,12 +135,12 @@ def cpu_baseline(lib, config, scene_key, w, h, spp, mb, threads, gpu_renderer=No
 
 
 # Oracle check in the CPU-baseline leg (the checker, never the measured
-# path): every k-th row of the bench frame rendered by the oracle (oracle/,
+# path): the bench frame (config 4: every 4th row) rendered by the oracle (oracle/,
 # the C restatement of the reference, OpenMP) and by the GPU from the same
 # seeds, compared bit for bit — RGBA8, frameSum and RNG state.  Config 5 is
 # left out: the oracle's brute-force loop over 10,256 primitives takes
 # minutes per row there (the GPU suite checks it against committed digests).
-ORACLE_ROW_STRIDE = {"c1": 1, "c2": 8, "c3": 8, "c4": 32}
+ORACLE_ROW_STRIDE = {"c1": 1, "c2": 1, "c3": 1, "c4": 4}
 
 
 def oracle_check(config, scene_key, w, h, spp, mb, gpu_renderer):
