@@ -4,6 +4,8 @@
 # ray-refill kernel — parity subset, kernel times, and one PMC pass per
 # candidate (L1 tag accesses, L1->L2 requests).  Run on the GPU box from the
 # repo root: tools/c5_coherent_ab.sh  -> gpurun_out/coh/
+# (round 6: the coherent-wave kernel lost 2.2x and was removed from the
+# source; to rerun, apply profiles/r06a/coherent_kernel.diff first)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 export BWRT_TUNING=1
 OUT=gpurun_out/coh; mkdir -p $OUT
