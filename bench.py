@@ -120,7 +120,11 @@ def cpu_baseline(lib, config, scene_key, w, h, spp, mb, threads, gpu_renderer=No
         dt = time.perf_counter() - t0
     rows = img.shape[0]
     out = {"value": round(rows * w * spp * mb / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads,
-           "kind": "fallback", "ms_per_sample": round(dt * 1e3, 2),
+           # a port of the reference's algorithm to scalar C++ (north_star's
+           # "scalar C++ CPU fallback of the same kernel"): the product's
+           # rt_render_cpu, bit-exact with the GPU and with the oracle
+           "kind": "port", "impl": "libbwrt.so rt_render_cpu (csrc/rt_cpu.cpp over csrc/rt_path.h)",
+           "ms_per_sample": round(dt * 1e3, 2),
            "sample": f"{'one full' if stride == 1 else f'rows y = 0 mod {stride} of one'} {w}x{h} {spp}-spp "
                      f"{mb}-bounce frame of scene {scene_key} ({rows} rows; libbwrt.so rt_render_cpu, "
                      f"{threads} threads; sched affinity {aff} CPUs, cgroup quota "

@@ -12,3 +12,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_c3 -o run --out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_c5 -o run --output-format csv -- \
     python3 bench.py --no-cpu-baseline --config c5 --steps 5 --warmup 2 > $O/rocprof_c5_bench.log 2>&1 || exit 1
 echo done > $O/done.txt
+# the triangle distance skip (RT_CULL_DIST, build/variants/cd1): parity
+# subset, then config 3 and its shards against HEAD
+SUBSET="config3_07_full or config3_shards or random_scenes or quads or 07_small or pair_kernel_forced or global_records_forced" \
+    timeout -k 10 600 bash tools/ab.sh "cd1:cd1:" > $O/parity_cd1.txt 2>&1 || exit 1
+ROUNDS=3 MODE=bench timeout -k 10 400 bash tools/ab.sh "head:base:" "cd1:cd1:" > $O/ab_cd1_c3.txt 2>&1 || exit 1
+ROUNDS=2 MODE=shard STRIDES=2,4,8 timeout -k 10 300 bash tools/ab.sh "head:base:" "cd1:cd1:" > $O/ab_cd1_shards.txt 2>&1 || exit 1
+echo done2 > $O/done2.txt
