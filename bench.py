@@ -456,7 +456,7 @@ def main():
                 "issue_frac": round(v["insts_valu_per_launch"] / ks / inst_peak, 4),
                 "active_lanes_per_valu": round(v["active_lanes_per_valu"], 2),
                 "counters": traffic.get("source")}
-        if traffic and traffic.get("l1"):
+        if traffic and traffic.get("l1") and "bvh" in (launched or ""):
             # the BVH walk's bound: the L1's line throughput.
             # achieved = the launch's L1 tag accesses (one per distinct line
             # per wave-load) / the kernel's time; peak = 256 CUs x the

@@ -296,7 +296,6 @@ void cull_sphere(float* cs, const rt_vec3* verts, int nv, double scale) {
     cs[0] = cs[1] = cs[2] = 0.0f;
     cs[3] = INFINITY;
     if (nv != 3) return;
-    cs[-1] = INFINITY;  // triangles: Rc (the record's pad word), infinite = no distance skip
     double v[3][3];
     for (int k = 0; k < 3; k++) {
         v[k][0] = verts[k].x;
@@ -327,7 +326,6 @@ void cull_sphere(float* cs, const rt_vec3* verts, int nv, double scale) {
     cs[1] = (float)c[1];
     cs[2] = (float)c[2];
     cs[3] = (float)rc2;
-    cs[-1] = std::nextafter((float)rc, INFINITY);  // Rc, rounded up (the triangle record's pad word)
 }
 
 void compile_polygon(float* q, float* h, const rt_vec3* verts, int nv, const rt_material& m, double scale) {

@@ -376,57 +376,31 @@ RT_HD bool polygon_edges(cfloat_ptr q, int nv, f3 P) {
 // evaluation error, ~2^-22 |w|^2), and only for origins within the scene
 // scale (rt_context.cpp cull_sphere: the reference rejects every such
 // polygon).  NaN/inf rays compare false and are never culled.
-// RT_CULL_DIST (A/B): also skip a triangle whose cull sphere lies wholly
-// beyond the closest hit so far: every point the reference's tests can
-// accept is within Rc of the centre (rt_context.cpp cull_sphere), so a hit
-// at t has t |d| >= |w| - Rc - (rounding of P = o + t d); the skip needs
-// |w| (1 - 2^-12) > Rc (1 + 2^-12) + best_t |d| (1 + 2^-12) + max|o_i| 2^-12
-// (margins far beyond the rounding), best_t finite (a NaN or infinite
-// closest distance never skips) and a culled-class ray (cr.ok: no overflow)
-#ifndef RT_CULL_DIST
-#define RT_CULL_DIST 0
-#endif
 struct CullRay {
     float a, a_k;  // |d|^2, |d|^2 (1 - 2^-14)
     bool ok;       // max|o_i| <= K.cull_omax and max|d_i| <= K.cull_dmax
-#if RT_CULL_DIST
-    float len_k;   // |d| (1 + 2^-12), approximate sqrt with margin
-    float om_k;    // max|o_i| 2^-12
-#endif
 };
 
 RT_HD CullRay cull_ray(const rt_kparams& K, f3 o, f3 d, float a) {
     CullRay c;
     c.a = a;
     c.a_k = a * (1.0f - 6.103515625e-05f);
-    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-    c.ok = om <= K.cull_omax && fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z)) <= K.cull_dmax;
-#if RT_CULL_DIST
-    c.len_k = sqrtf(a) * (1.0f + 2.44140625e-04f);
-    c.om_k = om * 2.44140625e-04f;
-#endif
+    c.ok = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= K.cull_omax &&
+           fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z)) <= K.cull_dmax;
     return c;
 }
 
-RT_HD bool culled(cfloat_ptr cs, const CullRay& cr, f3 o, f3 d, float best_t = INFINITY) {
+RT_HD bool culled(cfloat_ptr cs, const CullRay& cr, f3 o, f3 d) {
     const float wx = cs[0] - o.x, wy = cs[1] - o.y, wz = cs[2] - o.z;
     const float ww = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
     const float pj = __builtin_fmaf(wx, d.x, __builtin_fmaf(wy, d.y, wz * d.z));
     const float lhs = __builtin_fmaf(-pj, pj, ww * cr.a_k);
-#if RT_CULL_DIST
-    // (cs[-1]: Rc itself, rounded up; triangles only — a quad's sphere is infinite)
-    const float s = cs[-1] * (1.0f + 2.44140625e-04f) + __builtin_fmaf(best_t, cr.len_k, cr.om_k);
-    const bool beyond = best_t < INFINITY && ww * (1.0f - 4.8828125e-04f) > s * s;
-    return cr.ok && (lhs > cs[3] * cr.a || beyond);
-#else
-    (void)best_t;
     return cr.ok && lhs > cs[3] * cr.a;
-#endif
 }
 
 RT_HD void polygon_test(const rt_kparams& K, cfloat_ptr q, int nv, f3 o, f3 d, int id, const CullRay& cr,
                         float& best_t, int& best_id) {
-    if (culled(q + (nv == 3 ? RT_TRI_CULL : RT_QUAD_CULL), cr, o, d, nv == 3 ? best_t : INFINITY)) return;
+    if (culled(q + (nv == 3 ? RT_TRI_CULL : RT_QUAD_CULL), cr, o, d)) return;
     RT_BRANCH_COUNT(K, 2);
     float nx = q[0], ny = q[1], nz = q[2], dd = q[3];
     float nd = nx * d.x + ny * d.y + nz * d.z;
