@@ -552,6 +552,33 @@ def test_deinterleave_kernel(bwrt_lib, monkeypatch, blocks):
         r.close()
 
 
+def test_context_stream_priority(bwrt_lib, monkeypatch):
+    """The context's own stream (rt_get_stream) runs at the device's highest
+    priority, so a render dispatches ahead of a gather overlapping it
+    (bench.py's pipelined N > 1 step); BWRT_STREAM_PRIO=0 gives a normal one."""
+    import ctypes as C
+    from bwrt import Renderer
+    hip = C.CDLL("libamdhip64.so")  # the runtime torch and libbwrt.so share
+    least, greatest = C.c_int(), C.c_int()
+    assert hip.hipDeviceGetStreamPriorityRange(C.byref(least), C.byref(greatest)) == 0
+
+    def prio(r):
+        p = C.c_int()
+        assert hip.hipStreamGetPriority(C.c_void_p(r.stream_handle()), C.byref(p)) == 0
+        return p.value
+
+    r = Renderer(0, lib=bwrt_lib)
+    try:
+        assert prio(r) == greatest.value
+    finally:
+        r.close()
+    r = _fresh_renderer(bwrt_lib, monkeypatch, BWRT_STREAM_PRIO=0)
+    try:
+        assert prio(r) == 0  # the default priority (hipStreamCreateWithFlags)
+    finally:
+        r.close()
+
+
 def test_render_device_into_torch_buffer(gpu, oracle):
     """rt_render_device into a torch-allocated device buffer on a torch stream
     (the bench / multi-GPU path) equals the host-buffer render."""
