@@ -14,10 +14,15 @@ Metric: Msamples/s (nominal) = W*H*spp*bounces / t / 1e6,
 ms/frame = ms_per_step.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
-                  [--no-cpu-baseline] [--cpu-threads T]
+                  [--no-cpu-baseline] [--cpu-threads T] [--dist] [--no-overlap]
 The CPU baseline is the library's scalar C++ fallback (rt_render_cpu) on
 every CPU of the process's affinity (or --cpu-threads), timed on rank 0 at
-N = 1 after the GPU steps, and checked bit-exact against the GPU.
+N = 1 after the GPU steps, and checked bit-exact against the GPU; in the same
+leg the oracle (oracle/, the checker) renders the bench frame (config 4: a
+row sample; config 5: none) and the GPU's frame, frameSum and RNG state
+must equal it bit for bit ("oracle_check", "verified").
+--dist takes the multi-rank code path (process group, gather, de-interleave,
+verify) at N = 1 too.
 N > 1: one rank per GPU over RCCL.  Under torch.distributed.run (WORLD_SIZE
 set) each process is one rank; a plain `python bench.py --gpus N` starts
 torch.distributed.run itself (N child ranks on 127.0.0.1) before touching
