@@ -3,7 +3,7 @@
 config-3 renders back to back on the context's stream, each followed by a
 50-us clock probe (tools/micro/clock_probe.hip: s_memtime ticks per
 s_memrealtime tick), so a trend in the per-launch time can be read against
-the GPU's clock.  usage: tools/clock_ramp.py [N_LAUNCHES] [--config c3]
+the GPU's clock.  usage: tools/clock_ramp.py [N_LAUNCHES] [--config c3] [--reseed-at K] [--pause-at K]
 """
 import argparse
 import ctypes as C
@@ -22,6 +22,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("n", nargs="?", type=int, default=60)
     ap.add_argument("--config", default="c3")
+    ap.add_argument("--reseed-at", type=int, default=-1,
+                    help="re-seed the RNG (y*W+x) before this launch: a transient that comes back is the RNG's")
+    ap.add_argument("--pause-at", type=int, default=-1, help="idle the GPU 200 ms before this launch")
     a = ap.parse_args()
     probe = C.CDLL(os.path.join(REPO, "build", "libclockprobe.so"))
     probe.clock_probe_launch.argtypes = [C.c_void_p, C.c_uint, C.c_void_p]
@@ -38,7 +41,13 @@ def main():
     p = r.params(W, H, SPP, MB, first_frame=1)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.n)]
     torch.cuda.synchronize()
+    import time
     for i in range(a.n):
+        if i == a.reseed_at:
+            r.init_rand(W, H)  # (on the context's stream, ordered after the renders)
+        if i == a.pause_at:
+            torch.cuda.synchronize()
+            time.sleep(0.2)
         evs[i][0].record(stream)
         r.render_device(p, img.data_ptr(), stream.cuda_stream)
         evs[i][1].record(stream)
