@@ -287,6 +287,7 @@ def main():
     # the gather's landing buffers exist on the root only
     gathered = ([torch.empty((world, rows_per * W), dtype=torch.int32, device=dev) for _ in range(nbuf)]
                 if distributed and rank == 0 else [None] * nbuf)
+    torch.cuda.synchronize(dev)  # (the zero fills ran on torch's default stream, unordered with the renders)
     # the context's own stream (rt_get_stream), wrapped for torch: the
     # kernel, the bench's timing events and the RCCL gather are all ordered
     # on it, and renders on the context's stream defer the library's end

@@ -589,6 +589,7 @@ def test_render_device_into_torch_buffer(gpu, oracle):
     gpu.init_rand(w, h)
     buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
     stream = torch.cuda.Stream()
+    torch.cuda.synchronize()  # (the zero fill ran on torch's default stream, unordered with `stream`)
     gpu.render_device(gpu.params(w, h, 3, 4, first_frame=1), buf.data_ptr(), stream.cuda_stream)
     stream.synchronize()
     img = buf.cpu().numpy().view(np.uint8).reshape(h, w, 4)
@@ -611,6 +612,7 @@ def test_kernel_timing_off_and_on(gpu, oracle):
     st = oracle.OracleState(w, h)
     buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
     stream = torch.cuda.Stream()
+    torch.cuda.synchronize()  # (the zero fill ran on torch's default stream, unordered with `stream`)
     try:
         gpu.render(w, h, 1, mb, first_frame=1)
         assert gpu.last_kernel_ms() > 0
@@ -639,6 +641,7 @@ def test_state_writes_wait_for_device_render(gpu, oracle):
     s07, s04 = scenes.scene_07(), scenes.scene_04()
     stream = torch.cuda.Stream()
     buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # (the zero fill ran on torch's default stream, unordered with `stream`)
     seeds = oracle.OracleState(w, h)
     oracle.render(s07, seeds, 0, mb, first_frame=1)  # curand_init states only
     st = oracle.OracleState(w, h)
@@ -667,6 +670,7 @@ def test_state_writes_wait_for_device_render(gpu, oracle):
     # the last stream used, and that stream may be gone by the next write
     g = torch.zeros(h * w, dtype=torch.int32, device="cuda")
     out = torch.empty_like(g)
+    torch.cuda.synchronize()
     for _ in range(2):
         gpu.set_scene(s07)
         gpu.init_rand(w, h)
@@ -708,6 +712,7 @@ def test_context_stream_renders_defer_their_event(gpu, oracle):
     buf = torch.zeros(h * w, dtype=torch.int32, device="cuda")
     ctx_stream = torch.cuda.ExternalStream(gpu.stream_handle())
     other = torch.cuda.Stream()
+    torch.cuda.synchronize()  # (the zero fill ran on torch's default stream, unordered with these)
     gpu.set_kernel_timing(False)
     try:
         for f in (1, 3):  # frames 1-2, 3-4 on the context stream (handle, then NULL)
