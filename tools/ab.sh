@@ -8,6 +8,9 @@
 # MODE=shard  tools/shard_sweep.py --config $CONFIG --strides $STRIDES
 # SUBSET=expr first runs `pytest -m gpu -k expr` with every candidate library
 #             (the parity gate of an A/B; SUBSET=all: the whole GPU suite).
+# WARMUP=k    bench warm-up steps (default 3): a GPU idle between runs comes
+#             back through a ~20-launch power-management ramp (DESIGN.md §5,
+#             "Cold-start transient"); WARMUP=40 compares steady states
 # usage: ROUNDS=3 MODE=bench CONFIG=c3 bash tools/ab.sh "head:base:" "cand:myvar:"
 export BWRT_TUNING=1  # the library reads BWRT_* knobs only under it
 set -o pipefail
@@ -34,7 +37,7 @@ for r in $(seq ${ROUNDS:-3}); do
       grep stride $OUT/s_$label.log | sed "s/^/$label /"
     else
       env BWRT_LIB=$(lib_of $var) ${envs//,/ } timeout -k 10 200 python bench.py --no-cpu-baseline --config ${CONFIG:-c3} \
-          --steps ${STEPS:-20} --warmup 3 > $OUT/b_$label.log 2>&1 || { echo "$label failed"; tail -3 $OUT/b_$label.log; exit 1; }
+          --steps ${STEPS:-20} --warmup ${WARMUP:-3} > $OUT/b_$label.log 2>&1 || { echo "$label failed"; tail -3 $OUT/b_$label.log; exit 1; }
       echo "$label $(grep -o '"kernel_ms_avg[^,]*' $OUT/b_$label.log) $(grep -o '"ms_per_step[^,]*' $OUT/b_$label.log)"
     fi
   done
