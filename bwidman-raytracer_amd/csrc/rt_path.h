@@ -427,6 +427,11 @@ RT_HD void polygon_test(const rt_kparams& K, cfloat_ptr q, int nv, f3 o, f3 d, i
 // STEP = 2: only the indices i0, i0 + 2, ... (one half of a closest hit split
 // over two lanes, combined by key, rt_kernels.hip "split"; rays that pass
 // bvh_safe only)
+#ifndef RT_HIT_UNROLL  // A/B knob: unroll factor of the brute-force loop (the build's -fno-unroll-loops otherwise)
+#define RT_HIT_UNROLL 1
+#endif
+#define RT_PRAGMA(x) _Pragma(#x)
+#define RT_PRAGMA_UNROLL(n) RT_PRAGMA(unroll n)
 template <bool QUADS = true, int STEP = 1>
 RT_HD void closest_hit_brute(const rt_kparams& K, f3 o, f3 d, float& best_t, int& best_id, int i0 = 0) {
     const float a = dot(d, d);
@@ -439,6 +444,9 @@ RT_HD void closest_hit_brute(const rt_kparams& K, f3 o, f3 d, float& best_t, int
     const int quad_base = tri_base + K.n_tri;
     const CullRay cr = cull_ray(K, o, d, a);
     RT_BRANCH_COUNT(K, 4);
+#if RT_HIT_UNROLL > 1
+    RT_PRAGMA_UNROLL(RT_HIT_UNROLL)
+#endif
     for (int i = i0; i < K.n_max; i += STEP) {
         if (i < K.n_sph) {  // Intersection.cuh:15-62
             const cfloat_ptr s = as_const(K.sph) + RT_SPH_FLOATS * i;
