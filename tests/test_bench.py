@@ -125,3 +125,19 @@ def test_oracle_check_leg(bench, bwrt_lib):
     assert oc["bit_exact"] is True and oc["rows"] == 256 and oc["row_stride"] == 1
     assert bench.oracle_check("c5", "stress", 1920, 1080, 32, 8, None) is None
     assert set(bench.ORACLE_ROW_STRIDE) == {"c1", "c2", "c3", "c4"}
+
+
+def test_cpu_baseline_leg_repeats_sample(bench, bwrt_lib, monkeypatch):
+    """The CPU-baseline leg renders its sample again from the same seeds
+    (at least CPU_MIN_REPS times) and reports the median rep; handed a
+    renderer (here the CPU backend standing in for the GPU context) it
+    compares that renderer's frame with the sample, bit for bit."""
+    from bwrt import Renderer
+    monkeypatch.setattr(bench, "CPU_MIN_S", 0.0)
+    with Renderer.cpu(2, lib=bwrt_lib) as other:
+        other.set_scene(bench.scenes.SCENES["01"]())
+        out = bench.cpu_baseline(bwrt_lib, "c1", "01", 256, 256, 1, 1, 2, gpu_renderer=other)
+    assert out["reps"] == bench.CPU_MIN_REPS and out["cores"] == 2 and out["kind"] == "port"
+    lo, hi = out["ms_per_sample_min_max"]
+    assert lo <= out["ms_per_sample"] <= hi
+    assert out["bit_exact_vs_gpu"] is True and out["ms_per_frame"] == out["ms_per_sample"]
