@@ -1,4 +1,4 @@
-"""Multi-rank path on CPU (world_size 2 and 3, gloo): the interleaved-row
+"""Multi-rank path on CPU (world_size 2, 3 and 8, gloo): the interleaved-row
 shard plan, the padded gather of RGBA8 row blocks to rank 0 and the
 de-interleave that bench.py runs over RCCL.  Every rank renders its rows
 with the product — libbwrt.so's CPU backend (rt_create_cpu / rt_render_cpu,
@@ -49,7 +49,7 @@ def _worker(rank, world, port, w, h, spp, mb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("h,world", [(54, 2), (55, 2), (55, 3)])
+@pytest.mark.parametrize("h,world", [(54, 2), (55, 2), (55, 3), (30, 8)])
 def test_multi_rank_gather_matches_single_render(oracle, h, world):
     w, spp, mb = 96, 2, 4
     ctx = mp.get_context("spawn")
