@@ -113,6 +113,11 @@ __device__ __forceinline__ void closest_hit(const rt_kparams& K, f3 o, f3 d, flo
 #ifndef RT_NT_PIXEL
 #define RT_NT_PIXEL 3
 #endif
+// RT_NT_GREC (A/B knob, default 0): a global record's one read, at the path's
+// fold, non-temporal
+#ifndef RT_NT_GREC
+#define RT_NT_GREC 0
+#endif
 template <typename T>
 __device__ __forceinline__ T px_ld(const T* a) {
     if (RT_NT_PIXEL & 1) return __builtin_nontemporal_load(a);
@@ -605,7 +610,13 @@ rt_render_sorted_kernel(rt_kparams K) {
             if (GREC)
                 for (int l = nrec - 1; l >= LL; --l) {
                     const float* r = grec + 3 * (l - LL) * BLOCK;
+#if RT_NT_GREC
+                    // (the record's last read: non-temporal)
+                    fold_level(__float_as_int(x(__builtin_nontemporal_load(&r[0]))), x(__builtin_nontemporal_load(&r[BLOCK])),
+                               x(__builtin_nontemporal_load(&r[2 * BLOCK])), hit_tab, lx, ly, lz);
+#else
                     fold_level(__float_as_int(x(r[0])), x(r[BLOCK]), x(r[2 * BLOCK]), hit_tab, lx, ly, lz);
+#endif
                 }
             for (int l = (nrec < LL ? nrec : LL) - 1; l >= 0; --l) {
                 const lds_float* r = rec + 3 * l * BLOCK;
